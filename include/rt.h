@@ -1,0 +1,233 @@
+/*
+ * rt.h — C-ABI of the MI355X-native per-pixel ray-trace path.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (alp-aydin/Raytracing-Project).  Every entry point is plain C: pointers,
+ * sizes and integer error codes, no C++ types, no exceptions, no torch types.
+ *
+ * Reference seams replaced (paths relative to the reference repo root):
+ *   rt_scene_load_json_text  <- jsonio::load_scene_from_json_text
+ *                               raytracer/src/json_loader.cpp:458-490
+ *   rt_scene_load_json_file  <- jsonio::load_scene_from_json
+ *                               raytracer/src/json_loader.cpp:499-503
+ *   rt_render                <- Tracer::render (standard + paper mode)
+ *                               raytracer/src/tracer.cpp:247-305, tracer.h:18-35
+ *   rt_render_rows_device    <- the same loop restricted to a set of output
+ *                               rows (multi-GPU row tiling)
+ *   rt_scatter_rows_device   <- (no reference equivalent: places gathered row
+ *                               bands into the full framebuffer on rank 0)
+ *   rt_framebuffer_to_rgb8   <- framebuffer_to_mat_bgr8 / toByte
+ *                               raytracer/src/main.cpp:19-34, core.h:313-316
+ *   rt_write_png             <- cv::imwrite (main.cpp:86-89)
+ *
+ * The scene is held in a flattened intermediate representation
+ * (rt_scene_desc) produced by the host loader.  The same struct is consumed
+ * by the GPU renderer and by the CPU oracle under oracle/ (test only).
+ *
+ * Library split:
+ *   librt_host.so — loader, IR, PNG writer (pure host C++17, no HIP).
+ *   librtamd.so   — HIP/gfx950 renderer; links librt_host.so.
+ */
+#ifndef RT_H
+#define RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- errors */
+enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = -1,   /* null pointer / bad size                      */
+    RT_ERR_PARSE = -2,         /* "JSON parse error: ..." (json_loader.cpp:485) */
+    RT_ERR_PROCESSING = -3,    /* "JSON processing error: ..." (:487)          */
+    RT_ERR_IO = -4,            /* "Cannot open JSON file: ..." (:501) / PNG write */
+    RT_ERR_HIP = -5,           /* HIP runtime failure (message in rt_last_error) */
+    RT_ERR_UNSUPPORTED = -6,   /* scene exceeds a compiled device limit          */
+    RT_ERR_NO_DEVICE = -7      /* no HIP device / extension missing             */
+};
+
+/* Last error message of the calling thread ("" if none). */
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+/* -------------------------------------------------------- scene IR types */
+enum rt_node_kind {
+    RT_NODE_SPHERE = 0,       /* geometry.h:79-109     Sphere                    */
+    RT_NODE_HALFSPACE = 1,    /* geometry.h:112-158    HalfSpace                 */
+    RT_NODE_POKEBALL = 2,     /* geometry.h:161-242    Pokeball                  */
+    RT_NODE_TRANSLATION = 3,  /* transform.h:87-111    Translation               */
+    RT_NODE_SCALING = 4,      /* transform.h:117-141   Scaling                   */
+    RT_NODE_ROTATION = 5,     /* transform.h:150-185   Rotation                  */
+    RT_NODE_CSG = 6           /* csg.h:13-49           CSG                       */
+};
+
+enum rt_csg_op { RT_CSG_UNION = 0, RT_CSG_INTERSECTION = 1, RT_CSG_DIFFERENCE = 2 };
+
+enum rt_pokeball_region {
+    RT_PB_TOP = 0, RT_PB_BOTTOM = 1, RT_PB_BELT = 2, RT_PB_RING = 3, RT_PB_BUTTON = 4
+};
+
+/* Material — geometry.h:5-22.  Every JSON colour block instance (and each
+ * of a pokeball's five region materials) gets its own index: the paper-mode
+ * edge detector compares material identity (tracer.cpp:170). */
+typedef struct rt_material {
+    double albedo[3];
+    double ambient[3];
+    double kd, ks, kr, kt;
+    double shininess;
+    double refractive_index;
+} rt_material;
+
+/* Parameter layout of rt_node.v per kind:
+ *   SPHERE      v[0..2]=centre  v[3]=radius
+ *   HALFSPACE   v[0..2]=p0      v[3..5]=unit normal (normalised as geometry.h:124-134)
+ *   POKEBALL    v[0..2]=centre  v[3]=radius  v[4]=belt_half  v[5]=button_outer
+ *               v[6]=ring_width v[7..9]=unit button_dir (Dir3::normalized)
+ *   TRANSLATION/SCALING/ROTATION
+ *               v[0..11]  = forward matrix rows 0..2 (4 columns, row-major)
+ *               v[12..23] = inverse matrix rows 0..2 (Matrix4::inverse, core.h:239)
+ *   CSG         (no parameters; op in rt_node.op)
+ * aux[] keeps the raw constructor inputs (used only to rebuild reference
+ * objects in oracle/_ref): HALFSPACE aux[0..2]=normal as given,
+ * POKEBALL aux[0..2]=button_dir as given, ROTATION aux[0]=angle in radians,
+ * TRANSLATION/SCALING aux[0..2]=factors.
+ * Children: a (transform subject / CSG left), b (CSG right); -1 if unused.
+ * Materials: mat (sphere / halfspace), mats[5] (pokeball, rt_pokeball_region order). */
+typedef struct rt_node {
+    int32_t kind;
+    int32_t a, b;
+    int32_t op;        /* rt_csg_op for CSG; axis 0/1/2 for ROTATION */
+    int32_t mat;
+    int32_t mats[5];
+    double v[24];
+    double aux[4];
+} rt_node;
+
+typedef struct rt_light {      /* scene.h:21-26 PointLight */
+    double pos[3];
+    double intensity[3];
+} rt_light;
+
+typedef struct rt_camera {     /* camera.h:7-79 Camera + ScreenSpec */
+    double eye[3];
+    double P[3];
+    double Lx, Ly;
+    int32_t dpi;
+    int32_t pad_;
+} rt_camera;
+
+typedef struct rt_scene_desc {
+    rt_camera camera;
+    double background[3];      /* scene.h:40 */
+    double ambient[3];         /* scene.h:43 */
+    double medium_index;       /* scene.h:45 */
+    int32_t recursion_limit;   /* scene.h:47 (default 5) */
+    int32_t n_lights;
+    const rt_light* lights;
+    int32_t n_materials;
+    int32_t n_nodes;
+    const rt_material* materials;
+    const rt_node* nodes;
+    int32_t n_objects;         /* top-level objects, in JSON order */
+    int32_t pad_;
+    const int32_t* objects;    /* node index of each top-level object */
+} rt_scene_desc;
+
+/* ScreenSpec::nx/ny (camera.h:19-21): max(1, int(round(L * dpi))). */
+int rt_camera_width(const rt_camera* cam);
+int rt_camera_height(const rt_camera* cam);
+
+/* -------------------------------------------------------- scene handles */
+typedef struct rt_scene rt_scene;   /* opaque: owns the IR arrays */
+
+/* Parse JSON text with the reference schema.  On failure *out is NULL and
+ * rt_last_error() holds the message (same prefixes as the reference). */
+int rt_scene_load_json_text(const char* text, size_t len, rt_scene** out);
+int rt_scene_load_json_file(const char* path, rt_scene** out);
+/* Deep-copy a caller-built IR into an owned scene. */
+int rt_scene_from_desc(const rt_scene_desc* desc, rt_scene** out);
+const rt_scene_desc* rt_scene_get_desc(const rt_scene* s);
+void rt_scene_destroy(rt_scene* s);
+
+/* ------------------------------------------------------------- render */
+enum rt_mode { RT_MODE_STANDARD = 0, RT_MODE_PAPER = 1 };
+
+typedef struct rt_stats {
+    uint64_t rays_intersect;   /* Scene::intersect calls, reference definition (scene.cpp:10) */
+    uint64_t rays_occluded;    /* Scene::occluded calls (scene.cpp:33)                         */
+    uint64_t rays_traced;      /* intersect+occluded queries actually evaluated on device      */
+    uint64_t pixels;
+    double ms_rng;             /* jitter-stream generation (device)                             */
+    double ms_kernel;          /* trace kernels (device)                                        */
+    double ms_total;           /* whole call, host wall clock                                   */
+    uint64_t ops[16];          /* per-op counters when RT_FLAG_COUNT_OPS is set (rt_op_counter) */
+} rt_stats;
+
+/* Op counters used by the FLOP model. */
+enum rt_op_counter {
+    RT_OPC_SPHERE_ISECT = 0,    /* Sphere::intersect calls                 */
+    RT_OPC_SPHERE_ISECT_HIT,    /*   ... that hit                          */
+    RT_OPC_SPHERE_IVL,          /* Sphere::interval calls (incl. pokeball)  */
+    RT_OPC_SPHERE_IVL_HIT,      /*   ... that produced an interval         */
+    RT_OPC_HALF_ISECT,          /* HalfSpace::intersect calls              */
+    RT_OPC_HALF_ISECT_HIT,
+    RT_OPC_HALF_IVL,
+    RT_OPC_POKE_REGION,         /* Pokeball::pick_region_material          */
+    RT_OPC_CSG_COMBINE,         /* CSG::interval combine steps             */
+    RT_OPC_XFORM,               /* transform ray mappings                  */
+    RT_OPC_SHADE_LIGHT,         /* per-light shading evaluations           */
+    RT_OPC_SHADE_SPEC,          /* ... with a specular pow()               */
+    RT_OPC_SECONDARY,           /* reflection/refraction spawns            */
+    RT_OPC_CULLED,              /* subtree evaluations skipped by a wave-uniform bound cull */
+    RT_OPC_RESERVED0,
+    RT_OPC_RESERVED1
+};
+
+enum rt_flags {
+    RT_FLAG_NONE = 0,
+    RT_FLAG_COUNT_OPS = 1,      /* fill rt_stats.ops (slower, instrumented kernels) */
+    RT_FLAG_NO_CULL = 2         /* disable wave-uniform bounding-sphere culling    */
+};
+
+/* Tracer::render: render the whole frame into a caller-owned host buffer of
+ * W*H*3 doubles (row-major, top row first, RGB), exactly like the
+ * reference's std::vector<Color>.  W,H must be > 0 (the reference returns
+ * silently otherwise, tracer.cpp:248 — here RT_ERR_INVALID_ARG).
+ * Uses the current HIP device; blocks until done. */
+int rt_render(const rt_scene* s, int W, int H, int mode, int flags,
+              double* fb_host, rt_stats* stats);
+
+/* Render an arbitrary set of OUTPUT rows (top-row-first indices) into a
+ * compact device buffer fb_rows_dev[n_rows][W][3] on the given HIP stream
+ * (NULL = default stream).  rows_host lists the rows.  Blocks until done. */
+int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, int flags,
+                          const int32_t* rows_host, int n_rows,
+                          double* fb_rows_dev, void* hip_stream, rt_stats* stats);
+
+/* fb_dev[rows[i]][*] = src_dev[i][*] for i < n_rows (device copy, W*3 doubles per row). */
+int rt_scatter_rows_device(const double* src_dev, const int32_t* rows_dev, int n_rows,
+                           int W, double* fb_dev, void* hip_stream);
+
+/* Device-side toByte + RGB packing: rgb8_dev[W*H*3]. */
+int rt_framebuffer_to_rgb8_device(const double* fb_dev, size_t n_pixels,
+                                  uint8_t* rgb8_dev, void* hip_stream);
+
+/* ------------------------------------------------------------ host I/O */
+/* toByte(v) = round(clamp01(v)*255) (core.h:316), RGB order. */
+void rt_framebuffer_to_rgb8(const double* fb, size_t n_pixels, uint8_t* rgb8);
+/* Write an 8-bit RGB PNG (zlib deflate, n_threads > 1 parallelises the deflate). */
+int rt_write_png(const char* path, const uint8_t* rgb8, int W, int H, int n_threads);
+
+/* Number of HIP devices visible (0 when none / driver not loaded). */
+int rt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_H */

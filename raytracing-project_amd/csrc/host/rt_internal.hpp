@@ -1,0 +1,13 @@
+// rt_internal.hpp — helpers shared between librt_host and librtamd.
+#pragma once
+
+#include <string>
+
+#include "rt.h"
+
+namespace rtamd {
+void set_last_error(const std::string& msg);
+void clear_last_error();
+bool validate_desc(const rt_scene_desc& d, std::string* why);
+bool node_depth_ok(const rt_scene_desc& d, int idx, int level, int* maxdepth);
+}  // namespace rtamd

@@ -1,0 +1,326 @@
+"""rtamd — ctypes bindings over the C-ABI in include/rt.h.
+
+This is test/bench plumbing, not the product: the product is the C-ABI
+(lib/librtamd.so, lib/librt_host.so) and the `ray` CLI.  The Python names
+mirror the reference's interface for the hot path:
+
+* ``load_scene_from_json_text`` / ``load_scene_from_json`` ->
+  ``jsonio::load_scene_from_json_text`` / ``load_scene_from_json``
+  (raytracer/src/json_loader.cpp:458-503)
+* ``Tracer(scene, width, height, mode).render()`` -> ``Tracer::render``
+  (raytracer/src/tracer.h:18-35, tracer.cpp:247-305)
+
+The GPU path fails loudly (RuntimeError) when librtamd.so is missing or no HIP
+device is present; there is no CPU fallback.  The CPU oracle (oracle/) and the
+reference harness (oracle/_ref) are exposed separately for tests only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+BIN_DIR = os.path.join(PKG_DIR, "bin")
+ORACLE_DIR = os.path.join(REPO_DIR, "oracle")
+
+RT_OK = 0
+RT_MODE_STANDARD = 0
+RT_MODE_PAPER = 1
+RT_FLAG_NONE = 0
+RT_FLAG_COUNT_OPS = 1
+RT_FLAG_NO_CULL = 2
+
+NODE_SPHERE, NODE_HALFSPACE, NODE_POKEBALL, NODE_TRANSLATION, NODE_SCALING, NODE_ROTATION, NODE_CSG = range(7)
+CSG_UNION, CSG_INTERSECTION, CSG_DIFFERENCE = range(3)
+
+OP_NAMES = [
+    "sphere_isect", "sphere_isect_hit", "sphere_ivl", "sphere_ivl_hit", "half_isect", "half_isect_hit",
+    "half_ivl", "poke_region", "csg_combine", "xform", "shade_light", "shade_spec", "secondary", "culled",
+    "reserved0", "reserved1",
+]
+
+
+class Material(C.Structure):
+    _fields_ = [("albedo", C.c_double * 3), ("ambient", C.c_double * 3), ("kd", C.c_double), ("ks", C.c_double),
+                ("kr", C.c_double), ("kt", C.c_double), ("shininess", C.c_double),
+                ("refractive_index", C.c_double)]
+
+
+class Node(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("a", C.c_int32), ("b", C.c_int32), ("op", C.c_int32), ("mat", C.c_int32),
+                ("mats", C.c_int32 * 5), ("v", C.c_double * 24), ("aux", C.c_double * 4)]
+
+
+class Light(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("intensity", C.c_double * 3)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("eye", C.c_double * 3), ("P", C.c_double * 3), ("Lx", C.c_double), ("Ly", C.c_double),
+                ("dpi", C.c_int32), ("pad_", C.c_int32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("camera", Camera), ("background", C.c_double * 3), ("ambient", C.c_double * 3),
+                ("medium_index", C.c_double), ("recursion_limit", C.c_int32), ("n_lights", C.c_int32),
+                ("lights", C.POINTER(Light)), ("n_materials", C.c_int32), ("n_nodes", C.c_int32),
+                ("materials", C.POINTER(Material)), ("nodes", C.POINTER(Node)), ("n_objects", C.c_int32),
+                ("pad_", C.c_int32), ("objects", C.POINTER(C.c_int32))]
+
+
+class Stats(C.Structure):
+    _fields_ = [("rays_intersect", C.c_uint64), ("rays_occluded", C.c_uint64), ("rays_traced", C.c_uint64),
+                ("pixels", C.c_uint64), ("ms_rng", C.c_double), ("ms_kernel", C.c_double),
+                ("ms_total", C.c_double), ("ops", C.c_uint64 * 16)]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ops"}
+        d["ops"] = {OP_NAMES[i]: int(self.ops[i]) for i in range(16)}
+        return d
+
+
+class OracleStats(C.Structure):
+    _fields_ = [("rays_intersect", C.c_uint64), ("rays_occluded", C.c_uint64), ("ops", C.c_uint64 * 16)]
+
+
+class OracleHit(C.Structure):
+    _fields_ = [("t", C.c_double), ("p", C.c_double * 3), ("n", C.c_double * 3), ("mat", C.c_int32),
+                ("front_face", C.c_int32)]
+
+    def as_tuple(self):
+        return (self.t, tuple(self.p), tuple(self.n), self.mat, self.front_face)
+
+
+_dp = C.POINTER(C.c_double)
+
+
+def _load(path: str, mode=C.RTLD_GLOBAL):
+    if not os.path.exists(path):
+        raise RuntimeError(f"required library not built: {path} (run __graft_entry__.build())")
+    return C.CDLL(path, mode=mode)
+
+
+_host = None
+_amd = None
+_oracle = None
+_ref = None
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        lib = _load(os.path.join(LIB_DIR, "librt_host.so"))
+        lib.rt_last_error.restype = C.c_char_p
+        lib.rt_scene_load_json_text.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)]
+        lib.rt_scene_load_json_file.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
+        lib.rt_scene_from_desc.argtypes = [C.POINTER(SceneDesc), C.POINTER(C.c_void_p)]
+        lib.rt_scene_get_desc.argtypes = [C.c_void_p]
+        lib.rt_scene_get_desc.restype = C.POINTER(SceneDesc)
+        lib.rt_scene_destroy.argtypes = [C.c_void_p]
+        lib.rt_camera_width.argtypes = [C.POINTER(Camera)]
+        lib.rt_camera_height.argtypes = [C.POINTER(Camera)]
+        lib.rt_framebuffer_to_rgb8.argtypes = [_dp, C.c_size_t, C.POINTER(C.c_uint8)]
+        lib.rt_write_png.argtypes = [C.c_char_p, C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int]
+        _host = lib
+    return _host
+
+
+def amd_lib():
+    """The HIP renderer.  Raises if the extension is missing (no fallback)."""
+    global _amd
+    if _amd is None:
+        host_lib()
+        lib = _load(os.path.join(LIB_DIR, "librtamd.so"))
+        lib.rt_render.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, C.POINTER(Stats)]
+        lib.rt_render_rows_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                              C.POINTER(C.c_int32), C.c_int, C.c_void_p, C.c_void_p,
+                                              C.POINTER(Stats)]
+        lib.rt_scatter_rows_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        lib.rt_framebuffer_to_rgb8_device.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
+        lib.rt_device_count.restype = C.c_int
+        _amd = lib
+    return _amd
+
+
+def oracle_lib():
+    """CPU oracle (TEST INFRASTRUCTURE ONLY)."""
+    global _oracle
+    if _oracle is None:
+        lib = _load(os.path.join(ORACLE_DIR, "liboracle.so"), mode=C.RTLD_LOCAL)
+        lib.oracle_render_rows.argtypes = [C.POINTER(SceneDesc), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp,
+                                           C.POINTER(OracleStats), C.c_int]
+        lib.oracle_node_intersect.argtypes = [C.POINTER(SceneDesc), C.c_int, _dp, _dp, C.c_double, C.c_double,
+                                              C.POINTER(OracleHit)]
+        lib.oracle_node_interval.argtypes = [C.POINTER(SceneDesc), C.c_int, _dp, _dp, _dp, _dp,
+                                             C.POINTER(OracleHit), C.POINTER(OracleHit)]
+        lib.oracle_scene_intersect.argtypes = [C.POINTER(SceneDesc), _dp, _dp, C.c_double, C.c_double,
+                                               C.POINTER(OracleHit)]
+        lib.oracle_scene_occluded.argtypes = [C.POINTER(SceneDesc), _dp, _dp, C.c_double, C.c_double]
+        lib.oracle_camera_ray.argtypes = [C.POINTER(SceneDesc), C.c_int, C.c_int, C.c_double, C.c_double, C.c_int,
+                                          _dp, _dp]
+        lib.oracle_jitter.argtypes = [C.c_uint64, C.c_uint64, _dp]
+        lib.oracle_mt_words.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
+        _oracle = lib
+    return _oracle
+
+
+def ref_lib():
+    """The reference's own sources compiled by oracle/Makefile (container only)."""
+    global _ref
+    if _ref is None:
+        lib = _load(os.path.join(ORACLE_DIR, "_ref", "libref.so"), mode=C.RTLD_LOCAL)
+        lib.ref_render.argtypes = [C.POINTER(SceneDesc), C.c_int, C.c_int, C.c_int, _dp, C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64)]
+        lib.ref_node_intersect_batch.argtypes = [C.POINTER(SceneDesc), C.c_int, C.c_int, _dp, _dp, C.c_double,
+                                                 C.c_double, C.POINTER(C.c_int), C.POINTER(OracleHit)]
+        lib.ref_node_interval_batch.argtypes = [C.POINTER(SceneDesc), C.c_int, C.c_int, _dp, _dp,
+                                                C.POINTER(C.c_int), _dp, _dp, C.POINTER(OracleHit),
+                                                C.POINTER(OracleHit)]
+        lib.ref_camera_ray.argtypes = [C.POINTER(SceneDesc), C.c_int, C.c_int, C.c_double, C.c_double, C.c_int,
+                                       _dp, _dp]
+        lib.ref_jitter.argtypes = [C.c_uint64, C.c_uint64, _dp]
+        lib.ref_mt_words.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
+        _ref = lib
+    return _ref
+
+
+class RTError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def last_error() -> str:
+    return host_lib().rt_last_error().decode("utf-8", "replace")
+
+
+class Scene:
+    """Owned rt_scene handle (scene IR)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def desc(self) -> SceneDesc:
+        return host_lib().rt_scene_get_desc(self._h).contents
+
+    @property
+    def desc_ptr(self):
+        return host_lib().rt_scene_get_desc(self._h)
+
+    @property
+    def width(self) -> int:
+        return host_lib().rt_camera_width(C.byref(self.desc.camera))
+
+    @property
+    def height(self) -> int:
+        return host_lib().rt_camera_height(C.byref(self.desc.camera))
+
+    def close(self):
+        if self._h and self._h.value:
+            host_lib().rt_scene_destroy(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def load_scene_from_json_text(text: str) -> Scene:
+    """jsonio::load_scene_from_json_text (json_loader.cpp:458); raises RTError."""
+    raw = text.encode("utf-8")
+    out = C.c_void_p()
+    rc = host_lib().rt_scene_load_json_text(raw, len(raw), C.byref(out))
+    if rc != RT_OK:
+        raise RTError(rc, last_error())
+    return Scene(out.value)
+
+
+def load_scene_from_json(path: str) -> Scene:
+    """jsonio::load_scene_from_json (json_loader.cpp:499)."""
+    out = C.c_void_p()
+    rc = host_lib().rt_scene_load_json_file(path.encode(), C.byref(out))
+    if rc != RT_OK:
+        raise RTError(rc, last_error())
+    return Scene(out.value)
+
+
+def scene_from_desc(desc: SceneDesc) -> Scene:
+    out = C.c_void_p()
+    rc = host_lib().rt_scene_from_desc(C.byref(desc), C.byref(out))
+    if rc != RT_OK:
+        raise RTError(rc, last_error())
+    return Scene(out.value)
+
+
+def device_count() -> int:
+    return int(amd_lib().rt_device_count())
+
+
+@dataclass
+class Tracer:
+    """Mirror of the reference's Tracer (tracer.h:18-35) over the GPU C-ABI."""
+    scene: Scene
+    width: int
+    height: int
+    mode: int = RT_MODE_STANDARD
+    flags: int = RT_FLAG_NONE
+
+    def render(self, stats: Stats | None = None) -> np.ndarray:
+        lib = amd_lib()
+        fb = np.zeros((self.height, self.width, 3), dtype=np.float64)
+        st = stats if stats is not None else Stats()
+        rc = lib.rt_render(self.scene.handle, self.width, self.height, self.mode, self.flags,
+                           fb.ctypes.data_as(_dp), C.byref(st))
+        if rc != RT_OK:
+            raise RTError(rc, last_error())
+        return fb
+
+
+def oracle_render(scene: Scene, width: int, height: int, mode: int, row0: int = 0, row1: int | None = None,
+                  threads: int = 1):
+    """CPU oracle restricted to output rows [row0,row1).  TEST ONLY."""
+    if row1 is None:
+        row1 = height
+    fb = np.zeros((row1 - row0, width, 3), dtype=np.float64)
+    st = OracleStats()
+    rc = oracle_lib().oracle_render_rows(scene.desc_ptr, width, height, mode, row0, row1, fb.ctypes.data_as(_dp),
+                                         C.byref(st), threads)
+    if rc != 0:
+        raise RuntimeError("oracle_render_rows failed")
+    return fb, st
+
+
+def ref_render(scene: Scene, width: int, height: int, mode: int):
+    """The reference's own Tracer::render (oracle/_ref, container only)."""
+    fb = np.zeros((height, width, 3), dtype=np.float64)
+    ni, no = C.c_uint64(), C.c_uint64()
+    ref_lib().ref_render(scene.desc_ptr, width, height, mode, fb.ctypes.data_as(_dp), C.byref(ni), C.byref(no))
+    return fb, int(ni.value), int(no.value)
+
+
+def to_rgb8(fb: np.ndarray) -> np.ndarray:
+    fb = np.ascontiguousarray(fb, dtype=np.float64)
+    out = np.zeros(fb.shape, dtype=np.uint8)
+    host_lib().rt_framebuffer_to_rgb8(fb.ctypes.data_as(_dp), fb.size // 3, out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out
+
+
+def write_png(path: str, rgb8: np.ndarray, threads: int = 1) -> None:
+    rgb8 = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    h, w = rgb8.shape[:2]
+    rc = host_lib().rt_write_png(path.encode(), rgb8.ctypes.data_as(C.POINTER(C.c_uint8)), w, h, threads)
+    if rc != RT_OK:
+        raise RTError(rc, f"rt_write_png failed ({rc})")
