@@ -1,0 +1,95 @@
+// ray.cpp — drop-in CLI: ray <scene.json> <output.png> [--paper] [options]
+//
+// Mirrors raytracer/src/main.cpp:42-94: same usage text, same argv handling
+// (paper mode iff argv[3] == "--paper"), same exit codes
+// (1 usage, 2 load returned false, 3 exception while loading, 4 PNG write
+// failure) and the same final "Wrote <out> (WxH)[ (paper mode)]" line.
+// Extra options may follow argv[3] (the reference ignores them):
+//   --stats        print one JSON line with ray counts and timings
+//   --threads N    deflate threads for the PNG writer (default 8)
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "rt.h"
+#include "tracer.hpp"
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        std::cerr << "Usage: " << argv[0] << " <scene.json> <output.png> [--paper]\n";
+        std::cerr << "  --paper: Enable paper rendering mode with crosshatching\n";
+        return 1;
+    }
+    const std::string json_path = argv[1];
+    const std::string out_path = argv[2];
+    bool paper_mode = false;
+    if (argc > 3 && std::string(argv[3]) == "--paper") paper_mode = true;
+    bool print_stats = false;
+    int png_threads = 8;
+    for (int i = 3; i < argc; ++i) {
+        if (!std::strcmp(argv[i], "--stats")) print_stats = true;
+        else if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) png_threads = std::atoi(argv[++i]);
+    }
+
+    rtamd::Scene scene;
+    rtamd::Camera cam;
+    try {
+        if (!rtamd::jsonio::load_scene_from_json(json_path, scene, cam)) {
+            std::cerr << "Failed to load scene from " << json_path << "\n";
+            return 2;
+        }
+    } catch (const std::exception& e) {
+        std::cerr << "[error] " << e.what() << "\n";
+        return 3;
+    }
+
+    const int W = cam.nx();
+    const int H = cam.ny();
+    rtamd::Tracer tracer;
+    tracer.scene = &scene;
+    tracer.camera = &cam;
+    tracer.width = W;
+    tracer.height = H;
+    tracer.mode = paper_mode ? rtamd::RenderMode::Paper : rtamd::RenderMode::Standard;
+
+    if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
+    else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";
+    std::vector<rtamd::Color> framebuffer;
+    const auto t0 = std::chrono::steady_clock::now();
+    try {
+        tracer.render(framebuffer);
+    } catch (const std::exception& e) {
+        std::cerr << "[error] " << e.what() << "\n";
+        return 5;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    std::cout << "Rendering complete!\n";
+
+    std::vector<uint8_t> rgb((size_t)W * H * 3);
+    rt_framebuffer_to_rgb8(reinterpret_cast<const double*>(framebuffer.data()), (size_t)W * H, rgb.data());
+    const auto t2 = std::chrono::steady_clock::now();
+    if (rt_write_png(out_path.c_str(), rgb.data(), W, H, png_threads) != RT_OK) {
+        std::cerr << "Failed to write PNG: " << out_path << "\n";
+        return 4;
+    }
+    const auto t3 = std::chrono::steady_clock::now();
+    std::string mode_str = paper_mode ? " (paper mode)" : "";
+    std::cout << "Wrote " << out_path << " (" << W << "x" << H << ")" << mode_str << "\n";
+    if (print_stats) {
+        const rt_stats& s = tracer.stats;
+        const double ms_render = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        const double ms_png = std::chrono::duration<double, std::milli>(t3 - t1).count();
+        const double rays = (double)(s.rays_intersect + s.rays_occluded);
+        std::printf(
+            "{\"rays_intersect\": %llu, \"rays_occluded\": %llu, \"rays_traced\": %llu, \"ms_rng\": %.3f, "
+            "\"ms_kernel\": %.3f, \"ms_render\": %.3f, \"ms_png\": %.3f, \"mrays_per_s\": %.3f}\n",
+            (unsigned long long)s.rays_intersect, (unsigned long long)s.rays_occluded,
+            (unsigned long long)s.rays_traced, s.ms_rng, s.ms_kernel, ms_render, ms_png,
+            rays / (ms_render * 1e3));
+        (void)t2;
+    }
+    return 0;
+}

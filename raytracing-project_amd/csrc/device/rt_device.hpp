@@ -1,0 +1,847 @@
+// rt_device.hpp — FP64 device restatement of the reference trace path for
+// gfx950 (CDNA4).  Operation order follows the reference step for step and
+// the file is compiled with -ffp-contract=off and IEEE div/sqrt, so every
+// rounding matches the x86-64 reference except pow()/acos(), which come from
+// the device math library (<= 1 ulp apart).  Citations are
+// raytracer/src/<file>:<line> of the reference.
+//
+// Design:
+//   * one lane per (pixel, sample); a wave is 8 pixels x 8 samples,
+//   * the scene object loop and the per-object op programs are WAVE-UNIFORM:
+//     every lane walks the same sequence, parameters come through the scalar
+//     cache, and whole objects are skipped with __any() on a bound test,
+//   * transforms / CSG operands live on a ray stack and an interval stack
+//     whose top two intervals stay in VGPRs (left-deep folds never spill),
+//   * reflection / refraction recursion is an explicit per-lane frame stack.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt.h"
+#include "scene_compile.hpp"
+
+namespace rtd {
+
+using rtamd::DevObj;
+using rtamd::DevOp;
+
+constexpr double kEPS = 1e-6;   // core.h:10
+#define RT_INF __builtin_inf()
+
+constexpr int kMaxRayStack = 8;   // transform nesting (checked on the host)
+constexpr int kMaxIvlSpill = 6;   // interval stack entries beyond the top two
+constexpr int kMaxDepth = 16;     // recursion frames (medium.recursion <= 16)
+
+struct V3 {
+    double x, y, z;
+};
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ double dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b : a; }   // std::max
+__device__ __forceinline__ double dmin(double a, double b) { return (b < a) ? b : a; }   // std::min
+__device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+
+// Dir3::normalized (core.h:95-101)
+__device__ __forceinline__ V3 normalized(V3 v) {
+    double L = __builtin_sqrt(dot3(v, v));
+    if (L > kEPS) return v3(v.x / L, v.y / L, v.z / L);
+    return v3(0.0, 1.0, 0.0);
+}
+
+struct DRay {
+    V3 o, d;
+};
+// Ray::Ray (core.h:278) normalises the direction.
+__device__ __forceinline__ DRay make_ray(V3 o, V3 d) { return DRay{o, normalized(d)}; }
+__device__ __forceinline__ V3 ray_at(const DRay& r, double t) {   // core.h:280
+    return v3(r.o.x + r.d.x * t, r.o.y + r.d.y * t, r.o.z + r.d.z * t);
+}
+
+// Hit without t (interval hits' t is never observed: see DESIGN.md).
+struct DHit {
+    V3 p, n;
+    int mat;
+    int ff;
+};
+
+// Hit::set_face_normal (geometry.h:42-45)
+__device__ __forceinline__ void set_face_normal(DHit& h, const DRay& r, V3 outward) {
+    h.ff = dot3(r.d, outward) < 0.0;
+    h.n = h.ff ? outward : vneg(outward);
+}
+
+struct Ivl {
+    int ok;
+    double t0, t1;
+    DHit h0, h1;
+};
+
+struct THit {   // intersect-mode hit
+    int ok;
+    double t;
+    DHit h;
+};
+
+// Per-lane op counters (RT_FLAG_COUNT_OPS builds only).
+template <bool C>
+struct Cnt;
+template <>
+struct Cnt<false> {
+    __device__ __forceinline__ void inc(int) {}
+};
+template <>
+struct Cnt<true> {
+    uint32_t c[16];
+    __device__ __forceinline__ Cnt() {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = 0;
+    }
+    __device__ __forceinline__ void inc(int k) { c[k]++; }
+};
+
+struct DevScene {
+    const rt_node* nodes;
+    const rt_material* mats;
+    const rt_light* lights;
+    const DevObj* objs;
+    const DevOp* ops;
+    int n_lights, n_objs;
+    int cam_nx, cam_ny;
+    int rec_limit, cull;
+    double eye[3], P[3], Lx, Ly;
+    double bg[3], amb[3], medium_index;
+};
+
+__device__ __forceinline__ V3 ld3(const double* p) { return v3(p[0], p[1], p[2]); }
+
+// --------------------------------------------------------------- primitives
+// Sphere::intersect (geometry.cpp:12-37)
+template <class CT>
+__device__ __forceinline__ bool sphere_intersect(V3 c, double rad, const DRay& ray, double tmin, double tmax,
+                                                 double& t_out, DHit& out, CT& cnt) {
+    cnt.inc(RT_OPC_SPHERE_ISECT);
+    V3 oc = v3(ray.o.x - c.x, ray.o.y - c.y, ray.o.z - c.z);
+    double half_b = dot3(oc, ray.d);
+    double cterm = dot3(oc, oc) - rad * rad;
+    double disc = half_b * half_b - 1.0 * cterm;
+    if (disc < 0.0) return false;
+    double sq = __builtin_sqrt(disc);
+    double t = (-half_b - sq) / 1.0;
+    if (t < tmin || t > tmax) {
+        t = (-half_b + sq) / 1.0;
+        if (t < tmin || t > tmax) return false;
+    }
+    cnt.inc(RT_OPC_SPHERE_ISECT_HIT);
+    t_out = t;
+    out.p = ray_at(ray, t);
+    V3 outward = v3((out.p.x - c.x) / rad, (out.p.y - c.y) / rad, (out.p.z - c.z) / rad);
+    set_face_normal(out, ray, outward);
+    return true;
+}
+
+// Sphere::interval (geometry.cpp:48-78)
+template <class CT>
+__device__ __forceinline__ void sphere_interval(V3 c, double r, int mat, const DRay& ray, Ivl& o, CT& cnt) {
+    cnt.inc(RT_OPC_SPHERE_IVL);
+    V3 oc = v3(ray.o.x - c.x, ray.o.y - c.y, ray.o.z - c.z);
+    double half_b = dot3(oc, ray.d);
+    double cterm = dot3(oc, oc) - r * r;
+    double disc = half_b * half_b - 1.0 * cterm;
+    o.ok = !(disc < 0.0);
+    if (!o.ok) return;
+    cnt.inc(RT_OPC_SPHERE_IVL_HIT);
+    double s = __builtin_sqrt(disc);
+    double t0 = (-half_b - s) / 1.0;
+    double t1 = (-half_b + s) / 1.0;
+    if (t0 > t1) {
+        double tt = t0;
+        t0 = t1;
+        t1 = tt;
+    }
+    o.t0 = t0;
+    o.t1 = t1;
+    o.h0.p = ray_at(ray, t0);
+    set_face_normal(o.h0, ray, v3((o.h0.p.x - c.x) / r, (o.h0.p.y - c.y) / r, (o.h0.p.z - c.z) / r));
+    o.h0.mat = mat;
+    o.h1.p = ray_at(ray, t1);
+    set_face_normal(o.h1, ray, v3((o.h1.p.x - c.x) / r, (o.h1.p.y - c.y) / r, (o.h1.p.z - c.z) / r));
+    o.h1.mat = mat;
+}
+
+// HalfSpace::intersect (geometry.cpp:90-106)
+template <class CT>
+__device__ __forceinline__ bool half_intersect(V3 p0, V3 n, const DRay& r, double tmin, double tmax, double& t_out,
+                                               DHit& out, CT& cnt) {
+    cnt.inc(RT_OPC_HALF_ISECT);
+    const double ndotd = dot3(n, r.d);
+    if (__builtin_fabs(ndotd) < 1e-12) return false;
+    V3 diff = v3(p0.x - r.o.x, p0.y - r.o.y, p0.z - r.o.z);
+    const double t = dot3(n, diff) / ndotd;
+    if (t < tmin || t > tmax) return false;
+    cnt.inc(RT_OPC_HALF_ISECT_HIT);
+    t_out = t;
+    out.p = ray_at(r, t);
+    set_face_normal(out, r, n);
+    return true;
+}
+
+// HalfSpace::interval (geometry.cpp:117-147)
+template <class CT>
+__device__ __forceinline__ void half_interval(V3 p0, V3 n, int mat, const DRay& r, Ivl& o, CT& cnt) {
+    cnt.inc(RT_OPC_HALF_IVL);
+    const double ndotd = dot3(n, r.d);
+    V3 diff = v3(r.o.x - p0.x, r.o.y - p0.y, r.o.z - p0.z);
+    const double f0 = dot3(n, diff);
+    o.h0.mat = mat;
+    o.h1.mat = mat;
+    if (__builtin_fabs(ndotd) < 1e-12) {
+        o.ok = f0 >= 0.0;
+        o.t0 = -RT_INF;
+        o.t1 = RT_INF;
+        o.h0.p = r.o;
+        o.h1.p = r.o;
+    } else {
+        o.ok = 1;
+        const double tPlane = -f0 / ndotd;
+        if (ndotd > 0.0) {
+            o.t0 = tPlane;
+            o.t1 = RT_INF;
+            o.h0.p = ray_at(r, tPlane);
+            o.h1.p = r.o;
+        } else {
+            o.t0 = -RT_INF;
+            o.t1 = tPlane;
+            o.h0.p = r.o;
+            o.h1.p = ray_at(r, tPlane);
+        }
+    }
+    set_face_normal(o.h0, r, n);
+    set_face_normal(o.h1, r, n);
+}
+
+__device__ __forceinline__ double clamp1(double x) {   // geometry.cpp:152-156
+    if (x < -1.0) return -1.0;
+    if (x > 1.0) return 1.0;
+    return x;
+}
+
+// Pokeball::pick_region_material (geometry.cpp:163-180)
+template <class CT>
+__device__ __forceinline__ int pick_region(const rt_node* nd, V3 p, CT& cnt) {
+    cnt.inc(RT_OPC_POKE_REGION);
+    const double* v = nd->v;
+    const double r = v[3];
+    V3 u = v3((p.x - v[0]) / r, (p.y - v[1]) / r, (p.z - v[2]) / r);
+    const double ang = acos(clamp1(dot3(u, v3(v[7], v[8], v[9]))));
+    const double inner = dmax(0.0, v[5] - v[6]);
+    if (ang <= v[5]) return (ang >= inner) ? nd->mats[RT_PB_RING] : nd->mats[RT_PB_BUTTON];
+    if (__builtin_fabs(u.y) <= v[4]) return nd->mats[RT_PB_BELT];
+    return (u.y >= 0.0) ? nd->mats[RT_PB_TOP] : nd->mats[RT_PB_BOTTOM];
+}
+
+// Leaf Primitive::intersect for the three leaf kinds.
+template <class CT>
+__device__ __forceinline__ bool leaf_intersect(const rt_node* nd, const DRay& r, double tmin, double tmax,
+                                               double& t, DHit& h, CT& cnt) {
+    const int kind = nd->kind;
+    if (kind == RT_NODE_HALFSPACE) {
+        bool ok = half_intersect(ld3(nd->v), ld3(nd->v + 3), r, tmin, tmax, t, h, cnt);
+        h.mat = nd->mat;
+        return ok;
+    }
+    bool ok = sphere_intersect(ld3(nd->v), nd->v[3], r, tmin, tmax, t, h, cnt);
+    if (kind == RT_NODE_SPHERE) {
+        h.mat = nd->mat;
+    } else if (ok) {   // Pokeball::intersect (geometry.cpp:190-197)
+        h.mat = pick_region(nd, h.p, cnt);
+    }
+    return ok;
+}
+
+template <class CT>
+__device__ __forceinline__ void leaf_interval(const rt_node* nd, const DRay& r, Ivl& o, CT& cnt) {
+    const int kind = nd->kind;
+    if (kind == RT_NODE_HALFSPACE) {
+        half_interval(ld3(nd->v), ld3(nd->v + 3), nd->mat, r, o, cnt);
+        return;
+    }
+    sphere_interval(ld3(nd->v), nd->v[3], nd->mat, r, o, cnt);
+    if (kind == RT_NODE_POKEBALL && o.ok) {   // geometry.cpp:207-217
+        o.h0.mat = pick_region(nd, o.h0.p, cnt);
+        o.h1.mat = pick_region(nd, o.h1.p, cnt);
+    }
+}
+
+// ---------------------------------------------------------------- transforms
+// Matrix4 * Vec4 rows 0..2 (core.h:169-176)
+__device__ __forceinline__ V3 mat_apply(const double* m, V3 v, double w) {
+    return v3(m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3] * w, m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7] * w,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11] * w);
+}
+
+// Local ray of Translation / Scaling / Rotation (transform.cpp:24-29, 97-111, 184-196).
+// Degenerate Scaling never reaches the device (compiled to OP_NEVER).
+__device__ __forceinline__ DRay local_ray(const rt_node* nd, const DRay& r) {
+    const double* M = nd->v;
+    const int kind = nd->kind;
+    if (kind == RT_NODE_TRANSLATION) return make_ray(v3(r.o.x - M[3], r.o.y - M[7], r.o.z - M[11]), r.d);
+    if (kind == RT_NODE_SCALING) {
+        const double sx = M[0], sy = M[5], sz = M[10];
+        return make_ray(v3(r.o.x / sx, r.o.y / sy, r.o.z / sz), v3(r.d.x / sx, r.d.y / sy, r.d.z / sz));
+    }
+    const double* I = nd->v + 12;
+    return make_ray(mat_apply(I, r.o, 1.0), mat_apply(I, r.d, 0.0));
+}
+
+__device__ __forceinline__ V3 map_point(const rt_node* nd, V3 p) {
+    const double* M = nd->v;
+    const int kind = nd->kind;
+    if (kind == RT_NODE_TRANSLATION) return v3(p.x + M[3], p.y + M[7], p.z + M[11]);
+    if (kind == RT_NODE_SCALING) return v3(p.x * M[0], p.y * M[5], p.z * M[10]);
+    return mat_apply(M, p, 1.0);
+}
+
+__device__ __forceinline__ V3 map_normal(const rt_node* nd, V3 n) {
+    const double* M = nd->v;
+    const int kind = nd->kind;
+    if (kind == RT_NODE_TRANSLATION) return n;
+    if (kind == RT_NODE_SCALING) return normalized(v3(n.x / M[0], n.y / M[5], n.z / M[10]));
+    return normalized(mat_apply(M, n, 0.0));
+}
+
+// Transform::project_t_world (transform.h:76-80)
+__device__ __forceinline__ double project_t_world(const DRay& r, V3 Pw) {
+    V3 v = v3(Pw.x - r.o.x, Pw.y - r.o.y, Pw.z - r.o.z);
+    const double dd = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
+    return dd > 0.0 ? (v.x * r.d.x + v.y * r.d.y + v.z * r.d.z) / dd : RT_INF;
+}
+
+// ------------------------------------------------------------------- CSG
+__device__ __forceinline__ bool csg_combine(int op, bool a, bool b) {
+    return op == RT_CSG_UNION ? (a || b) : op == RT_CSG_INTERSECTION ? (a && b) : (a && !b);
+}
+
+// event_less lambda (csg.cpp:87-92); code = who*2 + type (type 0 Enter, 1 Exit)
+__device__ __forceinline__ bool ev_less(double ta, int ca, double tb, int cb) {
+    if (__builtin_fabs(ta - tb) > 1e-6) return ta < tb;
+    const int tya = ca & 1, tyb = cb & 1;
+    if (tya != tyb) return tya == 0;
+    return (ca >> 1) < (cb >> 1);
+}
+
+__device__ __forceinline__ const DHit& sel_hit(int code, const Ivl& a, const Ivl& b) {
+    return code == 0 ? a.h0 : code == 1 ? a.h1 : code == 2 ? b.h0 : b.h1;
+}
+
+// CSG::interval (csg.cpp:61-163) on the two child intervals already computed.
+template <class CT>
+__device__ __forceinline__ void csg_interval(int op, const Ivl& A, const Ivl& B, const DRay& ray, Ivl& R,
+                                             CT& cnt) {
+    R.ok = 0;
+    if (!A.ok && !B.ok) return;
+    cnt.inc(RT_OPC_CSG_COMBINE);
+    // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
+    double et[4];
+    int ec[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        et[k] = 0.0;
+        ec[k] = 0;
+    }
+    int n = 0;
+    {
+        const bool p0 = A.ok && __builtin_isfinite(A.t0);
+        const bool p1 = A.ok && __builtin_isfinite(A.t1);
+        const bool p2 = B.ok && __builtin_isfinite(B.t0);
+        const bool p3 = B.ok && __builtin_isfinite(B.t1);
+        const double tv[4] = {A.t0, A.t1, B.t0, B.t1};
+        const bool pv[4] = {p0, p1, p2, p3};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool here = pv[e] && n == k;
+                et[k] = here ? tv[e] : et[k];
+                ec[k] = here ? e : ec[k];
+            }
+            n += pv[e] ? 1 : 0;
+        }
+    }
+    // libstdc++ __insertion_sort (stl_algo.h:1819-1871) with the non-strict
+    // comparator, unrolled over the fixed <= 4 slots.
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        if (i < n) {
+            const double vt = et[i];
+            const int vc = ec[i];
+            if (ev_less(vt, vc, et[0], ec[0])) {
+#pragma unroll
+                for (int k = i; k > 0; --k) {
+                    et[k] = et[k - 1];
+                    ec[k] = ec[k - 1];
+                }
+                et[0] = vt;
+                ec[0] = vc;
+            } else {
+                bool moving = true;
+                int last = i;
+#pragma unroll
+                for (int k = i; k > 0; --k) {
+                    // __unguarded_linear_insert: while (comp(val, *next)) shift
+                    if (moving && ev_less(vt, vc, et[k - 1], ec[k - 1])) {
+                        et[k] = et[k - 1];
+                        ec[k] = ec[k - 1];
+                        last = k - 1;
+                    } else {
+                        moving = false;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k == last) {
+                        et[k] = vt;
+                        ec[k] = vc;
+                    }
+                }
+            }
+        }
+    }
+    bool inA = A.ok && (A.t0 < 1e-6) && (A.t1 > 1e-6);
+    bool inB = B.ok && (B.t0 < 1e-6) && (B.t1 > 1e-6);
+    bool inR = csg_combine(op, inA, inB);
+    bool haveEnter = false;
+    int enterCode = -1, exitCode = -1;
+    bool flipE = false, flipX = false;
+    double tEnt = 0.0, tExt = RT_INF;
+    int originMat = -1;
+    if (inR) {
+        haveEnter = true;
+        originMat = (inA && A.h0.mat >= 0) ? A.h0.mat : (inB ? B.h0.mat : -1);
+    }
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < n && !done) {
+            const bool before = inR;
+            const int code = ec[k];
+            const bool enter = (code & 1) == 0;
+            if ((code >> 1) == 0) inA = enter;
+            else inB = enter;
+            const bool after = csg_combine(op, inA, inB);
+            if (!before && after) {
+                haveEnter = true;
+                tEnt = et[k];
+                enterCode = code;
+                flipE = (op == RT_CSG_DIFFERENCE) && code == 3;
+            } else if (before && !after) {
+                tExt = et[k];
+                exitCode = code;
+                flipX = (op == RT_CSG_DIFFERENCE) && code == 2;
+                done = true;
+            }
+            if (!done) inR = after;
+        }
+    }
+    if (!haveEnter || !__builtin_isfinite(tExt)) return;
+    R.ok = 1;
+    R.t0 = tEnt;
+    R.t1 = tExt;
+    if (enterCode < 0) {
+        R.h0.p = ray.o;
+        R.h0.n = v3(0.0, 0.0, 0.0);
+        R.h0.mat = originMat;
+        R.h0.ff = 1;
+    } else {
+        R.h0 = sel_hit(enterCode, A, B);
+        if (flipE) set_face_normal(R.h0, ray, vneg(R.h0.n));
+    }
+    R.h1 = sel_hit(exitCode, A, B);
+    if (flipX) set_face_normal(R.h1, ray, vneg(R.h1.n));
+}
+
+// ------------------------------------------------------------ interpreter
+struct IStack {
+    Ivl tos, nos;
+    Ivl spill[kMaxIvlSpill];
+    int sp;   // number of entries (wave-uniform)
+
+    __device__ __forceinline__ void push(const Ivl& v) {
+        if (sp >= 2) spill[sp - 2] = nos;
+        if (sp >= 1) nos = tos;
+        tos = v;
+        ++sp;
+    }
+    // replace the top two by r
+    __device__ __forceinline__ void reduce2(const Ivl& r) {
+        tos = r;
+        if (sp >= 3) nos = spill[sp - 3];
+        --sp;
+    }
+};
+
+// Evaluate one OBJ_PROG object: Primitive::intersect(root, ray, tmin, tmax).
+template <class CT>
+__device__ __noinline__ bool run_program(const DevScene& S, int pc0, int pc1, const DRay& world, double tmin,
+                                         double tmax, double& t_out, DHit& h_out, CT& cnt) {
+    DRay cur = world;
+    DRay rstk[kMaxRayStack];
+    int rsp = 0;
+    IStack st;
+    st.sp = 0;
+    THit hit;
+    hit.ok = 0;
+    hit.t = 0.0;
+    for (int pc = pc0; pc < pc1; ++pc) {
+        const DevOp op = S.ops[pc];
+        const rt_node* nd = &S.nodes[op.node];
+        const double lo = op.top == 1 ? tmin : 0.0;
+        const double hi = op.top == 1 ? tmax : RT_INF;
+        switch (op.op) {
+            case rtamd::OP_XPUSH:
+                cnt.inc(RT_OPC_XFORM);
+                rstk[rsp++] = cur;
+                cur = local_ray(nd, cur);
+                break;
+            case rtamd::OP_LEAF_IVL: {
+                Ivl v;
+                leaf_interval(nd, cur, v, cnt);
+                st.push(v);
+                break;
+            }
+            case rtamd::OP_CSG: {
+                Ivl r;
+                csg_interval(op.csg_op, st.nos, st.tos, cur, r, cnt);
+                st.reduce2(r);
+                break;
+            }
+            case rtamd::OP_XPOP_IVL: {
+                const DRay parent = rstk[--rsp];
+                Ivl& v = st.tos;
+                if (v.ok) {   // transform.cpp:55-82 (138-169, 224-255)
+                    v.h0.p = map_point(nd, v.h0.p);
+                    v.h1.p = map_point(nd, v.h1.p);
+                    const V3 nE = map_normal(nd, v.h0.n);
+                    const V3 nX = map_normal(nd, v.h1.n);
+                    set_face_normal(v.h0, parent, nE);
+                    set_face_normal(v.h1, parent, nX);
+                    v.t0 = project_t_world(parent, v.h0.p);
+                    v.t1 = project_t_world(parent, v.h1.p);
+                }
+                cur = parent;
+                break;
+            }
+            case rtamd::OP_LEAF_ISECT: {
+                double t = 0.0;
+                hit.ok = leaf_intersect(nd, cur, lo, hi, t, hit.h, cnt);
+                hit.t = t;
+                break;
+            }
+            case rtamd::OP_CSG_ISECT: {   // CSG::intersect (csg.cpp:169-185)
+                const Ivl& v = st.tos;
+                const double t = dmax(v.t0, lo);
+                hit.ok = v.ok && (t < v.t1 && t < hi);
+                hit.t = t;
+                hit.h = v.h0;
+                hit.h.p = v3(cur.o.x + cur.d.x * t, cur.o.y + cur.d.y * t, cur.o.z + cur.d.z * t);
+                st.sp -= 1;
+                break;
+            }
+            case rtamd::OP_XPOP_HIT: {   // transform.cpp:18-44 (95-127, 182-213)
+                const DRay parent = rstk[--rsp];
+                if (hit.ok) {
+                    const V3 wp = map_point(nd, hit.h.p);
+                    const V3 wn = map_normal(nd, hit.h.n);
+                    const double wt = project_t_world(parent, wp);
+                    hit.ok = (wt > lo && wt < hi);
+                    hit.h.p = wp;
+                    set_face_normal(hit.h, parent, wn);
+                    hit.t = wt;
+                }
+                cur = parent;
+                break;
+            }
+            case rtamd::OP_NEVER:
+            default:
+                if (op.top == 2) {
+                    Ivl v;
+                    v.ok = 0;
+                    st.push(v);
+                } else {
+                    hit.ok = 0;
+                }
+                break;
+        }
+    }
+    t_out = hit.t;
+    h_out = hit.h;
+    return hit.ok;
+}
+
+// Conservative test: can the ray's [tmin,tmax] segment touch the bound?
+__device__ __forceinline__ bool bound_touch(const DevObj& ob, const DRay& r, double tmin, double tmax) {
+    V3 oc = v3(r.o.x - ob.bc[0], r.o.y - ob.bc[1], r.o.z - ob.bc[2]);
+    const double b = dot3(oc, r.d);
+    const double c = dot3(oc, oc) - ob.br * ob.br;
+    const double disc = b * b - c;
+    if (disc < 0.0) return false;
+    const double s = __builtin_sqrt(disc);
+    const double t0 = -b - s, t1 = -b + s;
+    const double m0 = 1e-6 * (1.0 + __builtin_fabs(tmin));
+    const double m1 = 1e-6 * (1.0 + __builtin_fabs(tmax));
+    return !(t1 < tmin - m0) && !(t0 > tmax + m1);
+}
+
+// Primitive::intersect for top-level object o (Scene::intersect body, scene.cpp:18).
+template <class CT>
+__device__ __forceinline__ bool object_intersect(const DevScene& S, const DevObj& ob, const DRay& r, double tmin,
+                                                 double tmax, double& t, DHit& h, CT& cnt) {
+    if (ob.kind == rtamd::OBJ_PROG) return run_program(S, ob.pc0, ob.pc1, r, tmin, tmax, t, h, cnt);
+    return leaf_intersect(&S.nodes[ob.node], r, tmin, tmax, t, h, cnt);
+}
+
+// Scene::intersect (scene.cpp:10-24): closest hit, later objects win ties
+// exactly as in the reference (each object applies its own accept rule).
+template <class CT>
+__device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, double tmax, double& t_best,
+                                DHit& best, CT& cnt) {
+    bool any = false;
+    double closest = tmax;
+    for (int o = 0; o < S.n_objs; ++o) {
+        const DevObj ob = S.objs[o];
+        if (ob.kind == rtamd::OBJ_NEVER) continue;
+        if (ob.kind == rtamd::OBJ_PROG && ob.has_bound && S.cull) {
+            const bool need = bound_touch(ob, r, tmin, closest);
+            if (!__any(need)) {
+                cnt.inc(RT_OPC_CULLED);
+                continue;
+            }
+        }
+        double t;
+        DHit h;
+        if (object_intersect(S, ob, r, tmin, closest, t, h, cnt)) {
+            any = true;
+            closest = t;
+            best = h;
+            t_best = t;
+        }
+    }
+    return any;
+}
+
+// Scene::occluded (scene.cpp:33-42): any hit; per-lane early exit.
+template <class CT>
+__device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, double tmax, CT& cnt) {
+    bool hit = false;
+    for (int o = 0; o < S.n_objs; ++o) {
+        if (__all(hit)) break;
+        const DevObj ob = S.objs[o];
+        if (ob.kind == rtamd::OBJ_NEVER) continue;
+        if (ob.kind == rtamd::OBJ_PROG && ob.has_bound && S.cull) {
+            const bool need = !hit && bound_touch(ob, r, tmin, tmax);
+            if (!__any(need)) {
+                cnt.inc(RT_OPC_CULLED);
+                continue;
+            }
+        }
+        if (!hit) {
+            double t;
+            DHit h;
+            hit = object_intersect(S, ob, r, tmin, tmax, t, h, cnt);
+        }
+    }
+    return hit;
+}
+
+// ----------------------------------------------------------------- shading
+__device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
+    return v3(1.0 - (1.0 - a.x) * (1.0 - b.x), 1.0 - (1.0 - a.y) * (1.0 - b.y), 1.0 - (1.0 - a.z) * (1.0 - b.z));
+}
+
+// shade_lambert_phong (shading.cpp:31-138), point lights only (the loader
+// never populates directional lights).
+template <class CT>
+__device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
+    if (hit.mat < 0) return v3(1.0, 0.0, 1.0);
+    const rt_material* m = &S.mats[hit.mat];
+    const V3 n = hit.n;
+    V3 E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
+    const double eps = dmax(1e-3, 1e-4 * ht);
+    const double kd = m->kd, ks = m->ks, shin = m->shininess;
+    const V3 alb = ld3(m->albedo);
+    for (int li = 0; li < S.n_lights; ++li) {
+        const rt_light* L = &S.lights[li];
+        V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
+        double d2 = dot3(tl, tl);
+        if (d2 <= 0.01) d2 = 0.01;
+        const double dist = __builtin_sqrt(d2);
+        const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
+        const double ndotl = dmax(0.0, dot3(n, wi));
+        if (ndotl <= 0.0) continue;
+        const double max_t = dist - eps;
+        if (max_t <= eps) continue;
+        const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
+        const DRay sr = make_ray(so, wi);
+        ++n_occl;
+        if (scene_occluded(S, sr, eps, max_t, cnt)) continue;
+        cnt.inc(RT_OPC_SHADE_LIGHT);
+        const double ed = dmax(0.5, dist);
+        const double falloff = 1.0 / (ed * ed);
+        const double f2 = falloff * 2.0;
+        const V3 IL = v3(L->intensity[0] * f2, L->intensity[1] * f2, L->intensity[2] * f2);
+        const double sd = kd * ndotl * 1.5;
+        const V3 Ed = v3(alb.x * IL.x * sd, alb.y * IL.y * sd, alb.z * IL.z * sd);
+        V3 Es = v3(0.0, 0.0, 0.0);
+        if (ks > 0.0) {
+            cnt.inc(RT_OPC_SHADE_SPEC);
+            const V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
+                                        2.0 * dot3(n, wi) * n.z - wi.z));
+            const double rdotv = dmax(0.0, dot3(rr, wo));
+            const double spec = pow(rdotv, shin) * ks;
+            Es = v3(IL.x * spec, IL.y * spec, IL.z * spec);
+        }
+        E = combine(E, combine(Ed, Es));
+    }
+    E.x = dmin(1.5, E.x);
+    E.y = dmin(1.5, E.y);
+    E.z = dmin(1.5, E.z);
+    return E;
+}
+
+// ---------------------------------------------------------------- tracing
+struct Frame {
+    V3 total;
+    DRay refr;
+    int mat;
+    int stage;      // 0 = reflection child pending, 1 = refraction child pending
+    int want_refr;
+};
+
+// Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
+template <class CT>
+__device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+    Frame stk[kMaxDepth];
+    int sp = 0;
+    int depth = 0;
+    const int limit = S.rec_limit;
+    V3 ret;
+    for (;;) {
+        // ---- evaluate node (r, depth)
+        bool descend = false;
+        if (depth >= limit) {
+            ret = v3(0.0, 0.0, 0.0);
+        } else {
+            double ht = 0.0;
+            DHit h;
+            ++n_isect;
+            if (!scene_intersect(S, r, 1e-4, RT_INF, ht, h, cnt)) {
+                ret = v3(S.bg[0], S.bg[1], S.bg[2]);
+            } else {
+                const V3 wo = normalized(vneg(r.d));
+                const V3 direct = shade(S, ht, h, wo, n_occl, cnt);
+                if (h.mat < 0) {
+                    ret = direct;
+                } else {
+                    const rt_material* mat = &S.mats[h.mat];
+                    const bool can = depth < limit - 1;
+                    const bool want_refl = mat->kr > 0.0 && can;
+                    bool want_refr = false;
+                    DRay refr;
+                    if (mat->kt > 0.0 && can) {
+                        const double eta = h.ff ? (S.medium_index / mat->refractive_index)
+                                                : (mat->refractive_index / S.medium_index);
+                        const V3 inc = normalized(r.d);
+                        const double cos_i = -dot3(inc, h.n);   // tracer.cpp:100-104
+                        const double st2 = eta * eta * dmax(0.0, 1.0 - cos_i * cos_i);
+                        if (!(st2 >= 1.0)) {
+                            want_refr = true;
+                            const double cos_t = __builtin_sqrt(1.0 - st2);   // tracer.cpp:87-98
+                            const double k = eta * cos_i - cos_t;
+                            const V3 rd = normalized(v3(inc.x * eta + h.n.x * k, inc.y * eta + h.n.y * k,
+                                                        inc.z * eta + h.n.z * k));
+                            const V3 ro = h.ff ? v3(h.p.x - h.n.x * 1e-6, h.p.y - h.n.y * 1e-6, h.p.z - h.n.z * 1e-6)
+                                               : v3(h.p.x + h.n.x * 1e-6, h.p.y + h.n.y * 1e-6, h.p.z + h.n.z * 1e-6);
+                            refr = make_ray(ro, rd);
+                        }
+                    }
+                    if (want_refl || want_refr) {
+                        Frame f;
+                        f.total = direct;
+                        f.mat = h.mat;
+                        f.want_refr = want_refr;
+                        f.refr = refr;
+                        if (want_refl) {
+                            cnt.inc(RT_OPC_SECONDARY);
+                            const V3 inc = normalized(r.d);
+                            const double k = 2.0 * dot3(inc, h.n);   // reflect (tracer.cpp:76-78)
+                            const V3 rd = normalized(v3(inc.x - h.n.x * k, inc.y - h.n.y * k, inc.z - h.n.z * k));
+                            const V3 ro = h.ff ? v3(h.p.x + h.n.x * 1e-6, h.p.y + h.n.y * 1e-6, h.p.z + h.n.z * 1e-6)
+                                               : v3(h.p.x - h.n.x * 1e-6, h.p.y - h.n.y * 1e-6, h.p.z - h.n.z * 1e-6);
+                            f.stage = 0;
+                            stk[sp++] = f;
+                            r = make_ray(ro, rd);
+                        } else {
+                            cnt.inc(RT_OPC_SECONDARY);
+                            f.stage = 1;
+                            stk[sp++] = f;
+                            r = refr;
+                        }
+                        depth = sp;
+                        descend = true;
+                    } else {
+                        ret = direct;
+                    }
+                }
+            }
+        }
+        if (descend) continue;
+        // ---- unwind
+        bool resumed = false;
+        while (sp > 0) {
+            Frame& f = stk[sp - 1];
+            const rt_material* mat = &S.mats[f.mat];
+            if (f.stage == 0) {
+                f.total = combine(f.total, v3(ret.x * mat->kr, ret.y * mat->kr, ret.z * mat->kr));
+                if (f.want_refr) {
+                    cnt.inc(RT_OPC_SECONDARY);
+                    f.stage = 1;
+                    r = f.refr;
+                    depth = sp;
+                    resumed = true;
+                    break;
+                }
+                ret = f.total;
+                --sp;
+            } else {
+                f.total = combine(f.total, v3(ret.x * mat->kt, ret.y * mat->kt, ret.z * mat->kt));
+                ret = f.total;
+                --sp;
+            }
+        }
+        if (!resumed) return ret;
+    }
+}
+
+// ------------------------------------------------------------------ camera
+// Camera::generate_ray_subpixel (camera.h:68-78)
+__device__ __forceinline__ DRay gen_ray_subpixel(const DevScene& S, int i, int j, double dx, double dy) {
+    const double sx = (i + 0.5 + dx) / (double)S.cam_nx;
+    const double sy = (j + 0.5 + dy) / (double)S.cam_ny;
+    const V3 Sp = v3(S.P[0] + S.Lx * sx + 0.0 * sy, S.P[1] + 0.0 * sx + S.Ly * sy, S.P[2] + 0.0 * sx + 0.0 * sy);
+    const V3 e = ld3(S.eye);
+    return make_ray(e, normalized(v3(Sp.x - e.x, Sp.y - e.y, Sp.z - e.z)));
+}
+
+// Camera::generate_ray (camera.h:44-58)
+__device__ __forceinline__ DRay gen_ray(const DevScene& S, int i, int j) {
+    const int nx = S.cam_nx, ny = S.cam_ny;
+    const V3 e = ld3(S.eye);
+    if (i < 0 || i >= nx || j < 0 || j >= ny) return make_ray(e, v3(0.0, 0.0, -1.0));
+    const double sx = ((double)i + 0.5) / (double)nx;
+    const int jf = ny - 1 - j;
+    const double sy = ((double)jf + 0.5) / (double)ny;
+    const V3 Sp = v3(S.P[0] + S.Lx * sx + 0.0 * sy, S.P[1] + 0.0 * sx + S.Ly * sy, S.P[2] + 0.0 * sx + 0.0 * sy);
+    return make_ray(e, normalized(v3(Sp.x - e.x, Sp.y - e.y, Sp.z - e.z)));
+}
+
+}  // namespace rtd

@@ -1,0 +1,587 @@
+// rt_render.hip — gfx950 render kernels and the librtamd C-ABI.
+//
+// Standard mode (Tracer::render, tracer.cpp:282-300):
+//   k_std: one lane per (pixel, sample); a wave covers 4x2 pixels x 8 samples,
+//   a 256-thread block 8x4 pixels.  Samples are summed in order s = 0..7
+//   across the 8 lanes of a pixel (cross-lane shuffles), then x 1/8.
+// Paper mode (tracer.cpp:258-281):
+//   k_paper_primary: one lane per pixel: the primary intersect (shared by
+//   trace_paper, the centre probe and the four neighbour probes of
+//   get_edge_strength, which all re-trace identical rays) + shading.
+//   k_paper_finish: edge strength from the stored neighbour hits + hatch.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mt_jump.hpp"
+#include "mt_poly.hpp"
+#include "rt.h"
+#include "rt_device.hpp"
+#include "rt_internal.hpp"
+#include "scene_compile.hpp"
+
+using namespace rtd;
+
+namespace {
+
+constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
+constexpr int kJitterK = 1024;          // twist blocks per jitter segment
+
+struct StdParams {
+    int W, H;
+    int n_rows;
+    int jy0;
+    const int32_t* rows;
+    const double* jit;
+    double* fb;
+    unsigned long long* counters;
+};
+
+template <bool C>
+__device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
+    // wave reduction, one atomic per wave and counter
+    unsigned long long a = ni, b = no;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+    }
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        if (a) atomicAdd(&ctr[0], a);
+        if (b) atomicAdd(&ctr[1], b);
+    }
+    if constexpr (C) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            unsigned long long v = cnt.c[k];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0 && v) atomicAdd(&ctr[2 + k], v);
+        }
+    }
+}
+
+template <bool C>
+__global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int s = lane & 7;
+    const int pix = lane >> 3;
+    const int x = blockIdx.x * 8 + (wave & 1) * 4 + (pix & 3);
+    const int ri = blockIdx.y * 4 + (wave >> 1) * 2 + (pix >> 2);
+    const bool active = x < P.W && ri < P.n_rows;
+    uint32_t ni = 0, no = 0;
+    Cnt<C> cnt;
+    V3 c = v3(0.0, 0.0, 0.0);
+    if (active) {
+        const int r = P.rows[ri];
+        const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
+        const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)(y - P.jy0) * P.W + x) * 16 + 2 * s);
+        const DRay ray = gen_ray_subpixel(S, x, y, j.x, j.y);
+        c = trace(S, ray, ni, no, cnt);
+    }
+    // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
+    const int base = lane & ~7;
+    V3 acc = v3(0.0, 0.0, 0.0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const double cx = __shfl(c.x, base + k);
+        const double cy = __shfl(c.y, base + k);
+        const double cz = __shfl(c.z, base + k);
+        acc.x += cx;
+        acc.y += cy;
+        acc.z += cz;
+    }
+    if (active && s == 0) {
+        const double inv = 1.0 / (double)8;
+        double* o = P.fb + ((size_t)ri * P.W + x) * 3;
+        o[0] = acc.x * inv;
+        o[1] = acc.y * inv;
+        o[2] = acc.z * inv;
+    }
+    flush_counters(P.counters, ni, no, cnt);
+}
+
+struct PaperParams {
+    int W, H;
+    int n_ext;
+    int n_rows;
+    const int32_t* ext_rows;     // rows needing a primary hit
+    const int32_t* ext_shade;    // 1 = row is rendered by this call (shade it)
+    const int32_t* nbr;          // per rendered row: ext index of r-1, r, r+1 (-1 = outside frame)
+    const int32_t* rows;         // rendered rows
+    int* hit;                    // [n_ext*W]
+    int* mat;
+    double* t;
+    double* nx;
+    double* ny;
+    double* nz;
+    double* lum;
+    double* fb;
+    unsigned long long* counters;
+};
+
+template <bool C>
+__global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
+    // block 16x16 pixels, wave 8x8
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int ei = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < P.W && ei < P.n_ext;
+    uint32_t ni = 0, no = 0;
+    Cnt<C> cnt;
+    if (active) {
+        const int y = P.ext_rows[ei];
+        const DRay r = gen_ray(S, x, y);
+        double ht = 0.0;
+        DHit h;
+        ++ni;
+        const bool hits = scene_intersect(S, r, 1e-4, RT_INF, ht, h, cnt);
+        const size_t idx = (size_t)ei * P.W + x;
+        P.hit[idx] = hits ? 1 : 0;
+        P.t[idx] = ht;
+        P.nx[idx] = h.n.x;
+        P.ny[idx] = h.n.y;
+        P.nz[idx] = h.n.z;
+        P.mat[idx] = hits ? h.mat : -3;
+        if (P.ext_shade[ei]) {
+            // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
+            V3 base = v3(1.0, 1.0, 1.0);
+            if (hits) base = shade(S, ht, h, normalized(vneg(r.d)), no, cnt);
+            P.lum[idx] = 0.299 * base.x + 0.587 * base.y + 0.114 * base.z;
+        }
+    }
+    flush_counters(P.counters, ni, no, cnt);
+}
+
+// apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
+__device__ __forceinline__ double crosshatch(double lum, int x, int y) {
+    if (lum < 0.15) return 0.0;
+    const double darkness = 1.0 - lum;
+    const bool diag1 = ((x + y) % 4) < 1;
+    const bool diag2 = ((x - y) % 4) < 1;
+    const bool horizontal = (y % 4) < 1;
+    bool draw = false;
+    if (darkness > 0.8) draw = (diag1 && diag2) || horizontal;
+    else if (darkness > 0.65) draw = (diag1 && diag2) || (horizontal && ((x + y) % 3 == 0));
+    else if (darkness > 0.5) draw = (diag1 && diag2) || (horizontal && ((x + y) % 4 == 0));
+    else if (darkness > 0.35) draw = diag1 || (horizontal && ((x + y) % 3 == 0));
+    else if (darkness > 0.2) draw = diag1;
+    else if (darkness > 0.12) draw = diag1 && ((x + y) % 8) < 2;
+    return draw ? 0.0 : 1.0;
+}
+
+__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= P.W || ri >= P.n_rows) return;
+    const int y = P.rows[ri];
+    const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
+    const size_t ci = (size_t)e_c * P.W + x;
+    const bool ch = P.hit[ci] != 0;
+    const double ct = P.t[ci];
+    const V3 cn = v3(P.nx[ci], P.ny[ci], P.nz[ci]);
+    const int cm = P.mat[ci];
+    // get_edge_strength (tracer.cpp:133-178): neighbours (-1,0) (1,0) (0,-1) (0,1)
+    double maxEdge = 0.0;
+    int valid = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int dx = (i == 0) ? -1 : (i == 1) ? 1 : 0;
+        const int dy = (i == 2) ? -1 : (i == 3) ? 1 : 0;
+        const int nxp = x + dx, nyp = y + dy;
+        if (nxp < 0 || nxp >= P.W || nyp < 0 || nyp >= P.H) continue;
+        ++valid;
+        const int er = (dy < 0) ? e_up : (dy > 0) ? e_dn : e_c;
+        const size_t ni = (size_t)er * P.W + nxp;
+        const bool nh = P.hit[ni] != 0;
+        if (ch != nh) {
+            maxEdge = dmax(maxEdge, 0.9);
+            continue;
+        }
+        if (ch && nh) {
+            const double nt = P.t[ni];
+            const double minD = dmin(ct, nt), maxD = dmax(ct, nt);
+            if (minD > 1e-4 && maxD / minD > 3.0) maxEdge = dmax(maxEdge, 0.6);
+            const double nd = dot3(cn, v3(P.nx[ni], P.ny[ni], P.nz[ni]));
+            if (nd < 0.2) maxEdge = dmax(maxEdge, 0.5);
+            if (cm != P.mat[ni] && nd < 0.7) maxEdge = dmax(maxEdge, 0.3);
+        }
+    }
+    if (valid < 4) maxEdge *= 0.5;
+    const double edge = maxEdge;
+    V3 o;
+    if (edge > 0.8) {
+        o = v3(0.0, 0.0, 0.0);
+    } else if (edge > 0.5) {
+        o = v3(0.2, 0.2, 0.2);
+    } else {
+        const double h = crosshatch(P.lum[ci], x, y);
+        o = v3(h, h, h);
+        if (edge > 0.3) {
+            const double darken = (edge - 0.3) * 0.4;
+            o.x *= (1.0 - darken);
+            o.y *= (1.0 - darken);
+            o.z *= (1.0 - darken);
+        }
+    }
+    double* dst = P.fb + ((size_t)ri * P.W + x) * 3;
+    dst[0] = o.x;
+    dst[1] = o.y;
+    dst[2] = o.z;
+}
+
+__global__ void k_scatter_rows(const double* __restrict__ src, const int32_t* __restrict__ rows, int n_rows, int W,
+                               double* __restrict__ dst) {
+    const size_t row_len = (size_t)W * 3;
+    const size_t total = row_len * n_rows;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / row_len, k = i - r * row_len;
+        dst[(size_t)rows[r] * row_len + k] = src[i];
+    }
+}
+
+__global__ void k_to_rgb8(const double* __restrict__ fb, size_t n, uint8_t* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const double v = fb[i];
+        double c = (v < 1.0) ? v : 1.0;   // std::min(1.0, v)
+        c = (0.0 < c) ? c : 0.0;          // std::max(0.0, .)
+        out[i] = (uint8_t)(int)round(c * 255.0);   // round half away from zero (core.h:316)
+    }
+}
+
+// ------------------------------------------------------------ host side
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) {                                                                  \
+            rtamd::set_last_error(std::string(#expr) + " failed: " + hipGetErrorString(e_));     \
+            return RT_ERR_HIP;                                                                   \
+        }                                                                                        \
+    } while (0)
+
+// Growable device buffer.
+struct DBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        size_t want = bytes + bytes / 8 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Per-device workspace (one render at a time per device; guarded by a mutex).
+struct Workspace {
+    std::mutex mu;
+    DBuf nodes, mats, lights, objs, ops;
+    DBuf rows, jit, ckpt, polys, basewin, counters;
+    DBuf paper_i, paper_d, paper_aux, fb;
+    int polys_levels = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+Workspace& workspace(int dev) {
+    static std::mutex gm;
+    static std::vector<Workspace*> ws;
+    std::lock_guard<std::mutex> lk(gm);
+    if ((int)ws.size() <= dev) ws.resize(dev + 1, nullptr);
+    if (!ws[dev]) ws[dev] = new Workspace;
+    return *ws[dev];
+}
+
+template <class T>
+hipError_t upload(DBuf& b, const std::vector<T>& v, hipStream_t st) {
+    size_t bytes = v.size() * sizeof(T);
+    hipError_t e = b.ensure(bytes ? bytes : 16);
+    if (e != hipSuccess || !bytes) return e;
+    return hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, st);
+}
+
+int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
+                     double* fb_dev, hipStream_t st, rt_stats* stats) {
+    const auto t_start = std::chrono::steady_clock::now();
+    if (!s) { rtamd::set_last_error("rt_render: scene is NULL"); return RT_ERR_INVALID_ARG; }
+    if (W <= 0 || H <= 0) { rtamd::set_last_error("rt_render: W and H must be > 0"); return RT_ERR_INVALID_ARG; }
+    if (mode != RT_MODE_STANDARD && mode != RT_MODE_PAPER) { rtamd::set_last_error("rt_render: bad mode"); return RT_ERR_INVALID_ARG; }
+    if (n_rows < 0 || (n_rows > 0 && (!rows_host || !fb_dev))) { rtamd::set_last_error("rt_render: bad rows/fb"); return RT_ERR_INVALID_ARG; }
+    for (int i = 0; i < n_rows; ++i)
+        if (rows_host[i] < 0 || rows_host[i] >= H) { rtamd::set_last_error("rt_render: row out of range"); return RT_ERR_INVALID_ARG; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        rtamd::set_last_error("rt_render: no HIP device available");
+        return RT_ERR_NO_DEVICE;
+    }
+    const rt_scene_desc& d = *rt_scene_get_desc(s);
+    rtamd::CompiledScene cs;
+    try {
+        cs = rtamd::compile_scene(d);
+    } catch (const std::exception& e) {
+        rtamd::set_last_error(std::string("scene compile: ") + e.what());
+        return RT_ERR_INVALID_ARG;
+    }
+    if (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2) {
+        rtamd::set_last_error("scene nesting exceeds the device stacks (transforms <= 8, CSG operand depth <= 8)");
+        return RT_ERR_UNSUPPORTED;
+    }
+    bool secondary = false;
+    for (int i = 0; i < d.n_materials; ++i)
+        if (d.materials[i].kr > 0.0 || d.materials[i].kt > 0.0) secondary = true;
+    if (secondary && mode == RT_MODE_STANDARD && d.recursion_limit - 1 > kMaxDepth) {
+        rtamd::set_last_error("medium.recursion exceeds the device frame stack (17)");
+        return RT_ERR_UNSUPPORTED;
+    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    Workspace& ws = workspace(dev);
+    std::lock_guard<std::mutex> lk(ws.mu);
+    if (!ws.ev[0])
+        for (int i = 0; i < 4; ++i) HIP_TRY(hipEventCreate(&ws.ev[i]));
+
+    // --- upload the scene (a few KB)
+    std::vector<rt_node> nodes(d.nodes, d.nodes + d.n_nodes);
+    std::vector<rt_material> mats(d.materials, d.materials + d.n_materials);
+    std::vector<rt_light> lights(d.lights, d.lights + d.n_lights);
+    HIP_TRY(upload(ws.nodes, nodes, st));
+    HIP_TRY(upload(ws.mats, mats, st));
+    HIP_TRY(upload(ws.lights, lights, st));
+    HIP_TRY(upload(ws.objs, cs.objs, st));
+    HIP_TRY(upload(ws.ops, cs.ops, st));
+    HIP_TRY(ws.counters.ensure(kCounterWords * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(ws.counters.p, 0, kCounterWords * sizeof(unsigned long long), st));
+
+    DevScene S;
+    S.nodes = ws.nodes.as<rt_node>();
+    S.mats = ws.mats.as<rt_material>();
+    S.lights = ws.lights.as<rt_light>();
+    S.objs = ws.objs.as<DevObj>();
+    S.ops = ws.ops.as<DevOp>();
+    S.n_lights = d.n_lights;
+    S.n_objs = (int)cs.objs.size();
+    S.cam_nx = rt_camera_width(&d.camera);
+    S.cam_ny = rt_camera_height(&d.camera);
+    S.rec_limit = d.recursion_limit;
+    S.cull = (flags & RT_FLAG_NO_CULL) ? 0 : 1;
+    for (int i = 0; i < 3; ++i) {
+        S.eye[i] = d.camera.eye[i];
+        S.P[i] = d.camera.P[i];
+        S.bg[i] = d.background[i];
+        S.amb[i] = d.ambient[i];
+    }
+    S.Lx = d.camera.Lx;
+    S.Ly = d.camera.Ly;
+    S.medium_index = d.medium_index;
+    const bool count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
+    unsigned long long* ctr = ws.counters.as<unsigned long long>();
+
+    uint64_t logical_isect = 0;
+    if (n_rows > 0) {
+        std::vector<int32_t> rows(rows_host, rows_host + n_rows);
+        if (mode == RT_MODE_STANDARD) {
+            int y0 = H, y1 = -1;
+            for (int r : rows) {
+                int y = H - 1 - r;
+                y0 = std::min(y0, y);
+                y1 = std::max(y1, y);
+            }
+            const int64_t q0 = (int64_t)32 * W * y0, q1 = (int64_t)32 * W * (y1 + 1);
+            const int levels = rtamd::mt_levels_needed(kJitterK, q1);
+            if (ws.polys_levels < levels) {
+                std::vector<uint32_t> tab = rtamd::mt_jump_table(kJitterK, levels);
+                HIP_TRY(upload(ws.polys, tab, st));
+                uint32_t win[624];
+                rtamd::mt_first_window(12345u, win);
+                std::vector<uint32_t> w(win, win + 624);
+                HIP_TRY(upload(ws.basewin, w, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                ws.polys_levels = levels;
+            }
+            const int64_t nseg = rtamd::mt_num_segments(kJitterK, q0, q1);
+            HIP_TRY(ws.ckpt.ensure((size_t)nseg * 624 * sizeof(uint32_t)));
+            HIP_TRY(ws.jit.ensure((size_t)(q1 - q0) / 2 * sizeof(double)));
+            HIP_TRY(upload(ws.rows, rows, st));
+            HIP_TRY(hipEventRecord(ws.ev[0], st));
+            HIP_TRY(rtamd::mt_launch_jitter(ws.basewin.as<uint32_t>(), ws.polys.as<uint32_t>(), ws.polys_levels,
+                                            kJitterK, q0, q1, ws.ckpt.as<uint32_t>(), ws.jit.as<double>(), st));
+            HIP_TRY(hipEventRecord(ws.ev[1], st));
+            StdParams P;
+            P.W = W;
+            P.H = H;
+            P.n_rows = n_rows;
+            P.jy0 = y0;
+            P.rows = ws.rows.as<int32_t>();
+            P.jit = ws.jit.as<double>();
+            P.fb = fb_dev;
+            P.counters = ctr;
+            dim3 grid((W + 7) / 8, (n_rows + 3) / 4);
+            if (count_ops) hipLaunchKernelGGL(k_std<true>, grid, dim3(256), 0, st, S, P);
+            else hipLaunchKernelGGL(k_std<false>, grid, dim3(256), 0, st, S, P);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ws.ev[2], st));
+        } else {
+            // rows needing a primary hit: rendered rows and their vertical neighbours
+            std::vector<char> need(H, 0), shade_row(H, 0);
+            for (int r : rows) {
+                need[r] = 1;
+                shade_row[r] = 1;
+                if (r > 0) need[r - 1] = 1;
+                if (r + 1 < H) need[r + 1] = 1;
+            }
+            std::vector<int32_t> ext, ext_shade, pos(H, -1);
+            for (int r = 0; r < H; ++r)
+                if (need[r]) {
+                    pos[r] = (int)ext.size();
+                    ext.push_back(r);
+                    ext_shade.push_back(shade_row[r]);
+                }
+            std::vector<int32_t> nbr(3 * (size_t)n_rows);
+            for (int i = 0; i < n_rows; ++i) {
+                const int r = rows[i];
+                nbr[3 * i + 0] = r > 0 ? pos[r - 1] : -1;
+                nbr[3 * i + 1] = pos[r];
+                nbr[3 * i + 2] = r + 1 < H ? pos[r + 1] : -1;
+                // logical Scene::intersect calls: trace_paper + centre + valid neighbours
+                logical_isect += (uint64_t)W * 2 + (uint64_t)(W > 1 ? 2 * (W - 1) : 0) +
+                                 (uint64_t)W * ((r > 0) + (r + 1 < H));
+            }
+            const int n_ext = (int)ext.size();
+            std::vector<int32_t> ints;
+            ints.insert(ints.end(), ext.begin(), ext.end());
+            ints.insert(ints.end(), ext_shade.begin(), ext_shade.end());
+            ints.insert(ints.end(), nbr.begin(), nbr.end());
+            ints.insert(ints.end(), rows.begin(), rows.end());
+            HIP_TRY(upload(ws.paper_aux, ints, st));
+            const size_t npx = (size_t)n_ext * W;
+            HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
+            HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
+            PaperParams P;
+            P.W = W;
+            P.H = H;
+            P.n_ext = n_ext;
+            P.n_rows = n_rows;
+            const int32_t* aux = ws.paper_aux.as<int32_t>();
+            P.ext_rows = aux;
+            P.ext_shade = aux + n_ext;
+            P.nbr = aux + 2 * n_ext;
+            P.rows = aux + 2 * n_ext + 3 * (size_t)n_rows;
+            P.hit = ws.paper_i.as<int>();
+            P.mat = P.hit + npx;
+            double* dd = ws.paper_d.as<double>();
+            P.t = dd;
+            P.nx = dd + npx;
+            P.ny = dd + 2 * npx;
+            P.nz = dd + 3 * npx;
+            P.lum = dd + 4 * npx;
+            P.fb = fb_dev;
+            P.counters = ctr;
+            HIP_TRY(hipEventRecord(ws.ev[0], st));
+            HIP_TRY(hipEventRecord(ws.ev[1], st));
+            dim3 g1((W + 15) / 16, (n_ext + 15) / 16);
+            if (count_ops) hipLaunchKernelGGL(k_paper_primary<true>, g1, dim3(256), 0, st, S, P);
+            else hipLaunchKernelGGL(k_paper_primary<false>, g1, dim3(256), 0, st, S, P);
+            HIP_TRY(hipGetLastError());
+            dim3 g2((W + 63) / 64, (n_rows + 3) / 4);
+            hipLaunchKernelGGL(k_paper_finish, g2, dim3(256), 0, st, P);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(ws.ev[2], st));
+        }
+    } else {
+        HIP_TRY(hipEventRecord(ws.ev[0], st));
+        HIP_TRY(hipEventRecord(ws.ev[1], st));
+        HIP_TRY(hipEventRecord(ws.ev[2], st));
+    }
+    unsigned long long hc[kCounterWords];
+    HIP_TRY(hipMemcpyAsync(hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->rays_intersect = mode == RT_MODE_PAPER ? logical_isect : hc[0];
+        stats->rays_occluded = hc[1];
+        stats->rays_traced = hc[0] + hc[1];
+        stats->pixels = (uint64_t)n_rows * W;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ws.ev[0], ws.ev[1]) == hipSuccess) stats->ms_rng = ms;
+        if (hipEventElapsedTime(&ms, ws.ev[1], ws.ev[2]) == hipSuccess) stats->ms_kernel = ms;
+        for (int k = 0; k < 16; ++k) stats->ops[k] = hc[2 + k];
+        stats->ms_total =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C-ABI
+extern "C" int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host,
+                                     int n_rows, double* fb_rows_dev, void* hip_stream, rt_stats* stats) {
+    return render_rows_impl(s, W, H, mode, flags, rows_host, n_rows, fb_rows_dev, (hipStream_t)hip_stream, stats);
+}
+
+extern "C" int rt_render(const rt_scene* s, int W, int H, int mode, int flags, double* fb_host, rt_stats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!fb_host) { rtamd::set_last_error("rt_render: fb is NULL"); return RT_ERR_INVALID_ARG; }
+    if (W <= 0 || H <= 0) { rtamd::set_last_error("rt_render: W and H must be > 0"); return RT_ERR_INVALID_ARG; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        rtamd::set_last_error("rt_render: no HIP device available");
+        return RT_ERR_NO_DEVICE;
+    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::vector<int32_t> rows(H);
+    for (int r = 0; r < H; ++r) rows[r] = r;
+    static std::mutex fbm;
+    static DBuf fb;
+    std::lock_guard<std::mutex> lk(fbm);
+    const size_t bytes = (size_t)W * H * 3 * sizeof(double);
+    HIP_TRY(fb.ensure(bytes));
+    int rc = render_rows_impl(s, W, H, mode, flags, rows.data(), H, fb.as<double>(), nullptr, stats);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipMemcpy(fb_host, fb.p, bytes, hipMemcpyDeviceToHost));
+    if (stats)
+        stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+extern "C" int rt_scatter_rows_device(const double* src_dev, const int32_t* rows_dev, int n_rows, int W,
+                                      double* fb_dev, void* hip_stream) {
+    if (n_rows <= 0) return RT_OK;
+    if (!src_dev || !rows_dev || !fb_dev || W <= 0) { rtamd::set_last_error("rt_scatter_rows_device: bad args"); return RT_ERR_INVALID_ARG; }
+    const size_t total = (size_t)W * 3 * n_rows;
+    const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_scatter_rows, dim3(blocks), dim3(256), 0, (hipStream_t)hip_stream, src_dev, rows_dev, n_rows,
+                       W, fb_dev);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+extern "C" int rt_framebuffer_to_rgb8_device(const double* fb_dev, size_t n_pixels, uint8_t* rgb8_dev,
+                                             void* hip_stream) {
+    if (!n_pixels) return RT_OK;
+    if (!fb_dev || !rgb8_dev) { rtamd::set_last_error("rt_framebuffer_to_rgb8_device: NULL"); return RT_ERR_INVALID_ARG; }
+    const size_t n = n_pixels * 3;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_to_rgb8, dim3(blocks), dim3(256), 0, (hipStream_t)hip_stream, fb_dev, n, rgb8_dev);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}

@@ -1,0 +1,234 @@
+// scene_compile.cpp — IR -> device object table + wave-uniform programs.
+//
+// Bounds: every node gets a conservative bounding sphere in the frame of the
+// ray it is queried with, or "unbounded" (half-spaces and anything whose
+// result can extend along them), or "empty" (can never report an interval
+// or a hit: degenerate Scaling, transform.cpp:97).  The bound of a CSG node
+// follows from the reference's interval semantics (csg.cpp:61-163): a union
+// is inside only where a child is; an intersection only where BOTH are; a
+// difference only where A is; the result's events are child events or the
+// origin (which then lies inside a child).  A ray whose [tmin,tmax] segment
+// misses an inflated bound therefore gets "no hit" from that subtree, which
+// lets the device skip it when no lane of the wave needs it.
+#include "scene_compile.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+
+namespace rtamd {
+namespace {
+
+struct Bound {
+    enum Kind { Empty, Unbounded, Ball } kind = Unbounded;
+    double c[3] = {0, 0, 0};
+    double r = 0;
+};
+
+Bound ball(double x, double y, double z, double r) {
+    Bound b;
+    b.kind = Bound::Ball;
+    b.c[0] = x; b.c[1] = y; b.c[2] = z;
+    b.r = std::fabs(r);
+    return b;
+}
+
+Bound merge_union(const Bound& a, const Bound& b) {
+    if (a.kind == Bound::Empty) return b;
+    if (b.kind == Bound::Empty) return a;
+    if (a.kind == Bound::Unbounded || b.kind == Bound::Unbounded) return Bound{};
+    double d[3] = {b.c[0] - a.c[0], b.c[1] - a.c[1], b.c[2] - a.c[2]};
+    double dist = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    if (dist + b.r <= a.r) return a;
+    if (dist + a.r <= b.r) return b;
+    double R = 0.5 * (dist + a.r + b.r);
+    Bound o;
+    o.kind = Bound::Ball;
+    double k = (dist > 0) ? (R - a.r) / dist : 0.0;
+    for (int i = 0; i < 3; ++i) o.c[i] = a.c[i] + d[i] * k;
+    o.r = R;
+    return o;
+}
+
+bool is_degenerate_scaling(const rt_node& n) {
+    const double kEPS = 1e-6;   // core.h:10, checked at transform.cpp:97
+    return n.kind == RT_NODE_SCALING &&
+           (std::fabs(n.v[0]) < kEPS || std::fabs(n.v[5]) < kEPS || std::fabs(n.v[10]) < kEPS);
+}
+
+class Compiler {
+public:
+    explicit Compiler(const rt_scene_desc& d) : d_(d) {}
+
+    Bound bound(int idx, int level = 0) {
+        if (level > 4096) throw std::runtime_error("scene graph too deep");
+        const rt_node& n = d_.nodes[idx];
+        switch (n.kind) {
+            case RT_NODE_SPHERE:
+            case RT_NODE_POKEBALL:
+                return ball(n.v[0], n.v[1], n.v[2], n.v[3]);
+            case RT_NODE_HALFSPACE:
+                return Bound{};
+            case RT_NODE_TRANSLATION: {
+                Bound b = bound(n.a, level + 1);
+                if (b.kind != Bound::Ball) return b;
+                return ball(b.c[0] + n.v[3], b.c[1] + n.v[7], b.c[2] + n.v[11], b.r);
+            }
+            case RT_NODE_SCALING: {
+                if (is_degenerate_scaling(n)) { Bound e; e.kind = Bound::Empty; return e; }
+                Bound b = bound(n.a, level + 1);
+                if (b.kind != Bound::Ball) return b;
+                double s = std::max(std::fabs(n.v[0]), std::max(std::fabs(n.v[5]), std::fabs(n.v[10])));
+                return ball(b.c[0] * n.v[0], b.c[1] * n.v[5], b.c[2] * n.v[10], b.r * s);
+            }
+            case RT_NODE_ROTATION: {
+                Bound b = bound(n.a, level + 1);
+                if (b.kind != Bound::Ball) return b;
+                const double* M = n.v;
+                return ball(M[0] * b.c[0] + M[1] * b.c[1] + M[2] * b.c[2] + M[3],
+                            M[4] * b.c[0] + M[5] * b.c[1] + M[6] * b.c[2] + M[7],
+                            M[8] * b.c[0] + M[9] * b.c[1] + M[10] * b.c[2] + M[11], b.r);
+            }
+            case RT_NODE_CSG: {
+                Bound a = bound(n.a, level + 1), b = bound(n.b, level + 1);
+                if (n.op == RT_CSG_UNION) return merge_union(a, b);
+                if (n.op == RT_CSG_INTERSECTION) {
+                    if (a.kind == Bound::Empty || b.kind == Bound::Empty) { Bound e; e.kind = Bound::Empty; return e; }
+                    if (a.kind == Bound::Ball && b.kind == Bound::Ball) return a.r <= b.r ? a : b;
+                    if (a.kind == Bound::Ball) return a;
+                    if (b.kind == Bound::Ball) return b;
+                    return Bound{};
+                }
+                return a;   // difference: inside only where A is
+            }
+        }
+        throw std::runtime_error("unknown node kind");
+    }
+
+    void emit_isect(int idx, int top, int level) {
+        if (level > 4096) throw std::runtime_error("scene graph too deep");
+        const rt_node& n = d_.nodes[idx];
+        switch (n.kind) {
+            case RT_NODE_SPHERE:
+            case RT_NODE_HALFSPACE:
+            case RT_NODE_POKEBALL:
+                op(OP_LEAF_ISECT, idx, top);
+                return;
+            case RT_NODE_TRANSLATION:
+            case RT_NODE_SCALING:
+            case RT_NODE_ROTATION:
+                if (is_degenerate_scaling(n)) { op(OP_NEVER, idx, top); return; }
+                op(OP_XPUSH, idx, top);
+                ray_push();
+                emit_isect(n.a, 0, level + 1);
+                op(OP_XPOP_HIT, idx, top);
+                --rdepth_;
+                return;
+            case RT_NODE_CSG:
+                emit_ivl(idx, level + 1);
+                op(OP_CSG_ISECT, idx, top);
+                --idepth_;
+                return;
+        }
+        throw std::runtime_error("unknown node kind");
+    }
+
+    void emit_ivl(int idx, int level) {
+        if (level > 4096) throw std::runtime_error("scene graph too deep");
+        const rt_node& n = d_.nodes[idx];
+        switch (n.kind) {
+            case RT_NODE_SPHERE:
+            case RT_NODE_HALFSPACE:
+            case RT_NODE_POKEBALL:
+                op(OP_LEAF_IVL, idx, 0);
+                ivl_push();
+                return;
+            case RT_NODE_TRANSLATION:
+            case RT_NODE_SCALING:
+            case RT_NODE_ROTATION:
+                if (is_degenerate_scaling(n)) {
+                    op(OP_NEVER, idx, 2);   // top == 2: push an empty interval
+                    ivl_push();
+                    return;
+                }
+                op(OP_XPUSH, idx, 0);
+                ray_push();
+                emit_ivl(n.a, level + 1);
+                op(OP_XPOP_IVL, idx, 0);
+                --rdepth_;
+                return;
+            case RT_NODE_CSG: {
+                emit_ivl(n.a, level + 1);
+                emit_ivl(n.b, level + 1);
+                DevOp& o = op(OP_CSG, idx, 0);
+                o.csg_op = n.op;
+                --idepth_;   // two popped, one pushed
+                return;
+            }
+        }
+        throw std::runtime_error("unknown node kind");
+    }
+
+    CompiledScene run() {
+        CompiledScene cs;
+        ops_ = &cs.ops;
+        for (int i = 0; i < d_.n_objects; ++i) {
+            int idx = d_.objects[i];
+            const rt_node& n = d_.nodes[idx];
+            DevObj o{};
+            o.node = idx;
+            Bound b = bound(idx);
+            if (b.kind == Bound::Empty) {
+                o.kind = OBJ_NEVER;
+            } else if (n.kind == RT_NODE_SPHERE) {
+                o.kind = OBJ_SPHERE;
+            } else if (n.kind == RT_NODE_HALFSPACE) {
+                o.kind = OBJ_HALF;
+            } else if (n.kind == RT_NODE_POKEBALL) {
+                o.kind = OBJ_POKE;
+            } else {
+                o.kind = OBJ_PROG;
+                o.strict = 1;
+                o.pc0 = (int)cs.ops.size();
+                rdepth_ = idepth_ = 0;
+                emit_isect(idx, 1, 0);
+                o.pc1 = (int)cs.ops.size();
+            }
+            if (b.kind == Bound::Ball) {
+                o.has_bound = 1;
+                double mag = std::fabs(b.c[0]) + std::fabs(b.c[1]) + std::fabs(b.c[2]) + b.r;
+                for (int k = 0; k < 3; ++k) o.bc[k] = b.c[k];
+                o.br = b.r * (1.0 + 1e-7) + 1e-7 * (1.0 + mag);
+            }
+            cs.objs.push_back(o);
+        }
+        cs.max_ray_depth = max_r_;
+        cs.max_ivl_depth = max_i_;
+        return cs;
+    }
+
+private:
+    const rt_scene_desc& d_;
+    std::vector<DevOp>* ops_ = nullptr;
+    int rdepth_ = 0, idepth_ = 0, max_r_ = 0, max_i_ = 0;
+
+    DevOp& op(int code, int node, int top) {
+        DevOp o{};
+        o.op = code;
+        o.node = node;
+        o.top = top;
+        ops_->push_back(o);
+        return ops_->back();
+    }
+    void ray_push() { ++rdepth_; max_r_ = std::max(max_r_, rdepth_); }
+    void ivl_push() { ++idepth_; max_i_ = std::max(max_i_, idepth_); }
+};
+
+}  // namespace
+
+CompiledScene compile_scene(const rt_scene_desc& d) {
+    Compiler c(d);
+    return c.run();
+}
+
+}  // namespace rtamd

@@ -1,0 +1,234 @@
+"""Scene inputs: the BASELINE.json configs and torture scenes.
+
+Configs (BASELINE.json "configs"):
+  1  examples/penguin.json unchanged, 1200x900 (CPU reference path)
+  2  640x480 synthetic: 3 spheres + 1 halfSpace, 3 lights, recursion 1
+  3  1920x1080 examples/pokeballs.json, 5 lights, recursion 3
+  4  3840x2160 examples/snorlax.json (deep CSG), 5 lights, recursion 4
+  5  7680x4320 synthetic 64 spheres + floor, 8 lights, recursion 6, --paper
+
+Resize rule: dpi = W/4, dimensions = [4, H/dpi], screen
+re-centred on the original screen centre.  Every function returns JSON text
+in the reference schema (raytracer/src/json_loader.cpp).
+"""
+from __future__ import annotations
+
+import copy
+import json
+import math
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SCENE_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "tests", "golden", "scenes")
+
+PENGUIN_LIGHTS = [
+    {"position": [5, 6, 8], "intensity": [20, 20, 20]},
+    {"position": [-5, 6, 8], "intensity": [15, 15, 15]},
+    {"position": [0, 3, 7], "intensity": [12, 12, 12]},
+]
+
+
+def load_example(name: str) -> dict:
+    with open(os.path.join(SCENE_DIR, f"{name}.json")) as f:
+        return json.load(f)
+
+
+def resize(scene: dict, width: int, height: int) -> dict:
+    """Apply the resize rule: dpi = W/4, dims = [4, H/dpi], same screen centre."""
+    s = copy.deepcopy(scene)
+    scr = s["screen"]
+    dims = scr.get("dimensions", [1, 1])
+    P = scr["position"]
+    cx, cy = P[0] + dims[0] / 2.0, P[1] + dims[1] / 2.0
+    dpi = width // 4
+    Ly = height / dpi
+    scr["dpi"] = dpi
+    scr["dimensions"] = [4, Ly]
+    scr["position"] = [cx - 2.0, cy - Ly / 2.0, P[2]]
+    return s
+
+
+def with_dpi(scene: dict, dpi: int) -> dict:
+    """Same screen, different dpi (used to make small parity cases)."""
+    s = copy.deepcopy(scene)
+    s["screen"]["dpi"] = dpi
+    return s
+
+
+def cfg2_scene() -> dict:
+    return {
+        "screen": {"dpi": 160, "dimensions": [4, 3], "position": [-2, -1.5, 0], "observer": [0, 0, 5]},
+        "medium": {"ambient": [0.1, 0.1, 0.1], "index": 1.0, "recursion": 1},
+        "background": [0.2, 0.3, 0.5],
+        "sources": copy.deepcopy(PENGUIN_LIGHTS),
+        "objects": [
+            {"halfSpace": {"position": [0, -1, 0], "normal": [0, 1, 0],
+                           "color": {"diffuse": [0.6, 0.6, 0.6], "specular": [0.1, 0.1, 0.1], "shininess": 8}}},
+            {"sphere": {"position": [-1.2, 0, -2], "radius": 0.8,
+                        "color": {"diffuse": [0.9, 0.1, 0.1], "specular": [0.5, 0.5, 0.5], "shininess": 32}}},
+            {"sphere": {"position": [0, 0, -3], "radius": 1.0,
+                        "color": {"diffuse": [0.1, 0.8, 0.2], "reflected": [0.5, 0.5, 0.5], "shininess": 64}}},
+            {"sphere": {"position": [1.2, 0, -2], "radius": 0.8, "index": 1.5,
+                        "color": {"diffuse": [0.1, 0.2, 0.9], "refracted": [0.5, 0.5, 0.5], "shininess": 16}}},
+        ],
+    }
+
+
+def cfg3_scene() -> dict:
+    s = resize(load_example("pokeballs"), 1920, 1080)
+    s["medium"]["recursion"] = 3
+    return s
+
+
+def cfg4_scene() -> dict:
+    s = resize(load_example("snorlax"), 3840, 2160)
+    s["sources"] = s["sources"] + [
+        {"position": [0, 8, 2], "intensity": [20, 20, 20]},
+        {"position": [3, -1, 6], "intensity": [15, 15, 15]},
+    ]
+    s["medium"]["recursion"] = 4
+    return s
+
+
+def cfg5_scene() -> dict:
+    objs = [{"halfSpace": {"position": [0, -1.6, 0], "normal": [0, 1, 0],
+                           "color": {"diffuse": [0.6, 0.6, 0.6], "specular": [0.1, 0.1, 0.1], "shininess": 8}}}]
+    for k in range(64):
+        i, j = k % 8, k // 8
+        col = {"diffuse": [(i + 1) / 9.0, (j + 1) / 9.0, 0.5], "specular": [0.3, 0.3, 0.3],
+               "shininess": 16 + 8 * (k % 4)}
+        sph = {"position": [-3.5 + i, -1.2 + 0.35 * j, -2.0 - j], "radius": 0.3 + 0.05 * ((i + j) % 3), "color": col}
+        if k % 3 == 0:
+            col["reflected"] = [0.3, 0.3, 0.3]
+        if k % 5 == 0:
+            col["refracted"] = [0.4, 0.4, 0.4]
+            sph["index"] = 1.5
+        objs.append({"sphere": sph})
+    lights = [{"position": [6 * math.cos(2 * math.pi * l / 8), 6, 2 + 6 * math.sin(2 * math.pi * l / 8)],
+               "intensity": [20, 20, 20]} for l in range(8)]
+    return {
+        "screen": {"dpi": 1920, "dimensions": [4, 2.25], "position": [-2, -1.125, 0], "observer": [0, 0, 5]},
+        "medium": {"ambient": [0.1, 0.1, 0.1], "index": 1.0, "recursion": 6},
+        "background": [0.2, 0.3, 0.5],
+        "sources": lights,
+        "objects": objs,
+    }
+
+
+CONFIGS = {
+    1: ("penguin 1200x900 (config 1)", lambda: load_example("penguin"), 0),
+    2: ("synthetic 640x480 3 spheres + halfSpace, 3 lights, rec 1 (config 2)", cfg2_scene, 0),
+    3: ("pokeballs 1920x1080, 5 lights, rec 3 (config 3)", cfg3_scene, 0),
+    4: ("snorlax 3840x2160, 5 lights, rec 4 (config 4)", cfg4_scene, 0),
+    5: ("synthetic 7680x4320 64 spheres, 8 lights, rec 6, paper (config 5)", cfg5_scene, 1),
+}
+
+
+def config_json(n: int, dpi: int | None = None) -> tuple[str, int]:
+    """(json_text, mode) for config n, optionally at a reduced dpi."""
+    _, fn, mode = CONFIGS[n]
+    s = fn()
+    if dpi is not None:
+        s = with_dpi(s, dpi)
+    return json.dumps(s), mode
+
+
+# ------------------------------------------------------------- torture scenes
+def _mat(d, **kw):
+    m = {"diffuse": list(d), "ambient": [0.05, 0.05, 0.05], "specular": [0.4, 0.4, 0.4], "shininess": 24}
+    m.update(kw)
+    return m
+
+
+def _base(objects, recursion=3, dpi=24, lights=None):
+    return {
+        "screen": {"dpi": dpi, "dimensions": [4, 3], "position": [-2, -1.5, 0], "observer": [0, 0.3, 5]},
+        "medium": {"ambient": [0.2, 0.2, 0.2], "index": 1.0, "recursion": recursion},
+        "background": [0.3, 0.4, 0.6],
+        "sources": lights or copy.deepcopy(PENGUIN_LIGHTS),
+        "objects": objects,
+    }
+
+
+def torture_scenes(dpi: int = 24) -> dict[str, dict]:
+    """Scenes covering every node kind, the CSG/transform quirks and recursion."""
+    floor = {"halfSpace": {"position": [0, -1.2, 0], "normal": [0, 1, 0], "color": _mat([0.5, 0.6, 0.5])}}
+    sc = {}
+    sc["rotation_scaling"] = _base([
+        floor,
+        {"rotation": {"angle": 30, "direction": 1, "subject": {
+            "scaling": {"factors": [1.5, 0.6, 1.0], "subject": {
+                "sphere": {"position": [0, 0, 0], "radius": 0.8, "color": _mat([0.8, 0.3, 0.2])}}}}}},
+        {"rotation": {"angle": -45, "direction": 2, "subject": {
+            "translation": {"factors": [1.6, 0.2, -1.0], "subject": {
+                "sphere": {"position": [0, 0, 0], "radius": 0.5, "color": _mat([0.2, 0.3, 0.9])}}}}}},
+        {"rotation": {"angle": 60, "direction": 0, "subject": {
+            "sphere": {"position": [-1.6, 0.3, -1.5], "radius": 0.6, "color": _mat([0.9, 0.9, 0.2])}}}},
+    ], dpi=dpi)
+    sc["csg_ops"] = _base([
+        floor,
+        {"intersection": [
+            {"sphere": {"position": [-1.5, 0, -1], "radius": 0.9, "color": _mat([0.9, 0.2, 0.2])}},
+            {"sphere": {"position": [-1.0, 0, -1], "radius": 0.9, "color": _mat([0.2, 0.9, 0.2])}}]},
+        {"difference": [
+            {"sphere": {"position": [0.3, 0.2, -1.5], "radius": 1.0, "color": _mat([0.9, 0.8, 0.2])}},
+            {"sphere": {"position": [0.3, 0.2, -0.6], "radius": 0.6, "color": _mat([0.2, 0.2, 0.9])}},
+            {"sphere": {"position": [0.9, 0.8, -1.0], "radius": 0.4, "color": _mat([0.7, 0.2, 0.7])}}]},
+        {"csg": {"operator": "union",
+                 "left": {"sphere": {"position": [1.8, -0.4, -1], "radius": 0.5, "color": _mat([0.3, 0.7, 0.9])}},
+                 "right": {"union": [
+                     {"sphere": {"position": [1.8, 0.3, -1], "radius": 0.35, "color": _mat([0.9, 0.5, 0.1])}},
+                     {"sphere": {"position": [2.2, 0.0, -1], "radius": 0.3, "color": _mat([0.5, 0.9, 0.1])}}]}}},
+    ], dpi=dpi)
+    sc["halfspace_in_csg"] = _base([
+        {"intersection": [
+            {"sphere": {"position": [0, 0, -1.5], "radius": 1.2, "color": _mat([0.8, 0.4, 0.3])}},
+            {"halfSpace": {"position": [0, 0.2, 0], "normal": [0.3, -1, 0.2], "color": _mat([0.3, 0.8, 0.4])}}]},
+        {"difference": [
+            {"sphere": {"position": [1.7, 0.3, -1.0], "radius": 0.7, "color": _mat([0.4, 0.4, 0.9])}},
+            {"halfSpace": {"position": [1.7, 0.3, -1.0], "normal": [1, 1, 0], "color": _mat([0.9, 0.9, 0.9])}}]},
+        {"union": [
+            {"sphere": {"position": [-1.8, 0.0, -1.0], "radius": 0.5, "color": _mat([0.9, 0.9, 0.3])}},
+            {"halfSpace": {"position": [0, -1.3, 0], "normal": [0, 1, 0], "color": _mat([0.4, 0.5, 0.4])}}]},
+        {"translation": {"factors": [0.0, -0.2, 0.0], "subject": {
+            "halfSpace": {"position": [0, -1.0, -6], "normal": [0, 0, 1], "color": _mat([0.5, 0.5, 0.7])}}}},
+    ], dpi=dpi)
+    sc["pokeball_csg"] = _base([
+        floor,
+        {"pokeball": {"position": [-1.2, 0, -1], "radius": 0.8, "button_dir": [0.2, 0.1, 1.0]}},
+        {"difference": [
+            {"pokeball": {"position": [1.2, 0, -1], "radius": 0.8, "button_dir": [-0.3, 0.2, 1.0],
+                          "belt_half": 0.1, "button_outer": 0.35, "ring_width": 0.08}},
+            {"sphere": {"position": [1.6, 0.5, -0.4], "radius": 0.4, "color": _mat([0.2, 0.2, 0.2])}}]},
+        {"scaling": {"factors": [0.5, 0.5, 0.5], "subject": {
+            "pokeball": {"position": [0, -1.6, -1], "radius": 0.8}}}},
+    ], dpi=dpi)
+    sc["reflect_refract"] = _base([
+        floor,
+        {"sphere": {"position": [-1.2, 0, -1.5], "radius": 0.7,
+                    "color": _mat([0.2, 0.2, 0.2], reflected=[0.8, 0.8, 0.8])}},
+        {"sphere": {"position": [0.3, -0.1, -0.8], "radius": 0.6, "index": 1.5,
+                    "color": _mat([0.1, 0.1, 0.1], refracted=[0.9, 0.9, 0.9], reflected=[0.1, 0.1, 0.1])}},
+        {"sphere": {"position": [1.6, 0.1, -1.2], "radius": 0.5, "index": 2.4,
+                    "color": _mat([0.3, 0.1, 0.1], refracted=[0.7, 0.7, 0.7])}},
+        {"difference": [
+            {"sphere": {"position": [0.0, 1.0, -2.5], "radius": 0.6, "index": 1.3,
+                        "color": _mat([0.5, 0.5, 0.8], refracted=[0.6, 0.6, 0.6], reflected=[0.3, 0.3, 0.3])}},
+            {"sphere": {"position": [0.0, 1.0, -2.5], "radius": 0.3, "color": _mat([0.9, 0.2, 0.2])}}]},
+    ], recursion=6, dpi=dpi)
+    sc["recursion0"] = copy.deepcopy(sc["reflect_refract"])
+    sc["recursion0"]["medium"]["recursion"] = 0
+    sc["inside_camera"] = {
+        # eye inside a CSG union and inside a sphere: origin-inside paths (csg.cpp:113-122)
+        "screen": {"dpi": dpi, "dimensions": [4, 3], "position": [-2, -1.5, 0], "observer": [0, 0, 1]},
+        "medium": {"ambient": [0.3, 0.3, 0.3], "index": 1.0, "recursion": 2},
+        "background": [0.1, 0.1, 0.1],
+        "sources": [{"position": [0, 0.5, 0.5], "intensity": [5, 5, 5]}],
+        "objects": [
+            {"union": [
+                {"sphere": {"position": [0, 0, 1], "radius": 3.0, "color": _mat([0.6, 0.5, 0.4])}},
+                {"sphere": {"position": [0, 0, -3], "radius": 1.0, "color": _mat([0.2, 0.5, 0.4])}}]},
+            {"sphere": {"position": [0.5, 0, -1], "radius": 0.5, "color": _mat([0.9, 0.1, 0.1])}},
+        ],
+    }
+    return sc
