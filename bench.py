@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json headline metric on MI355X.
+
+Metric: Mrays/s (primary + secondary) and wall-clock per frame on config 4:
+examples/snorlax.json at 3840x2160, 5 lights, recursion 4.
+A "ray" is one Scene::intersect or Scene::occluded query of the reference
+(raytracer/src/scene.cpp:10,33).  A "step" renders one whole frame: jitter
+stream generation (mt19937 jump-ahead) + trace kernels, with the scene and
+all buffers resident on the device; for N > 1 each rank renders interleaved
+8-row strips of the SAME frame (strong scaling) and rank 0 receives all rows
+with one RCCL all_gather over xGMI and scatters them into the frame.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4]
+For N > 1 the driver launches one process per GPU with torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
+
+FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: 256 CU x 64 lanes x 2 x 2.4 GHz
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table
+STRIP = 8                      # rows per interleaved strip (multi-GPU)
+
+
+def model_flops(ops: dict, primary: int, paper: bool) -> tuple[float, dict]:
+    """Algorithmic FP64 FLOPs from executed-op counters, per SURVEY.md §8d's
+    table (+,-,*,/,sqrt = 1; pow/acos counted separately)."""
+    si, sih = ops["sphere_isect"], ops["sphere_isect_hit"]
+    sv, svh = ops["sphere_ivl"], ops["sphere_ivl_hit"]
+    hi, hih, hv = ops["half_isect"], ops["half_isect_hit"], ops["half_ivl"]
+    f = 17 * (si - sih) + 36 * sih + 17 * (sv - svh) + 54 * svh
+    f += 14 * (hi - hih) + 25 * hih + 30 * hv
+    f += 12 * ops["poke_region"] + 34 * ops["xform"]
+    f += (39 if paper else 51) * primary
+    f += 4 * ops["shade_call"]
+    occl = ops.get("_occluded", 0)
+    f += 17 * max(0, ops["light_eval"] - occl) + 33 * occl
+    f += 38 * (ops["shade_light"] - ops["shade_spec"]) + 80 * ops["shade_spec"]
+    f += 70 * ops["secondary"]
+    return float(f), {"pow": ops["shade_spec"], "acos": ops["poke_region"]}
+
+
+def strip_rows(H: int, rank: int, world: int) -> list[int]:
+    rows = []
+    for s in range((H + STRIP - 1) // STRIP):
+        if s % world == rank:
+            rows.extend(range(s * STRIP, min(H, (s + 1) * STRIP)))
+    return rows
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=4)
+    ap.add_argument("--cpu-rows", type=int, default=64, help="rows in the CPU-oracle baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cull", action="store_true", help="disable wave-uniform bound culling")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import rtamd
+    import scenes
+
+    text, mode = scenes.config_json(args.config)
+    sc = rtamd.load_scene_from_json_text(text)
+    W, H = sc.width, sc.height
+    lib = rtamd.amd_lib()
+    flags = rtamd.RT_FLAG_NO_CULL if args.no_cull else rtamd.RT_FLAG_NONE
+    dev = torch.device("cuda", local)
+
+    rows = strip_rows(H, rank, world)
+    n_rows = len(rows)
+    rows_c = (C.c_int32 * max(1, n_rows))(*rows)
+    max_rows = len(strip_rows(H, 0, world))
+    fb_rows = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)
+    full = torch.zeros((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
+    gathered = None
+    all_rows_dev = None
+    if world > 1:
+        gathered = torch.zeros((world * max_rows, W, 3), dtype=torch.float64, device=dev) if True else None
+        if rank == 0:
+            cat = []
+            for r in range(world):
+                rr = strip_rows(H, r, world)
+                cat.extend(rr + [-1] * (max_rows - len(rr)))
+            all_rows_dev = torch.tensor(cat, dtype=torch.int32, device=dev)
+
+    stream = torch.cuda.current_stream(dev)
+    st = rtamd.Stats()
+
+    def step(f=flags, stats=st):
+        rc = lib.rt_render_rows_device(sc.handle, W, H, mode, f, rows_c, n_rows, C.c_void_p(fb_rows.data_ptr()),
+                                       C.c_void_p(stream.cuda_stream), C.byref(stats))
+        if rc != 0:
+            raise RuntimeError(f"rt_render_rows_device failed ({rc}): {rtamd.last_error()}")
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, fb_rows)
+            if rank == 0:
+                # padded slots carry row -1: scatter only the real rows
+                for r in range(world):
+                    nr = len(strip_rows(H, r, world))
+                    lib.rt_scatter_rows_device(C.c_void_p(gathered[r * max_rows].data_ptr()),
+                                               C.c_void_p(all_rows_dev[r * max_rows:].data_ptr()), nr, W,
+                                               C.c_void_p(full.data_ptr()), C.c_void_p(stream.cuda_stream))
+        elif rank == 0:
+            lib.rt_scatter_rows_device(C.c_void_p(fb_rows.data_ptr()), C.c_void_p(0), 0, W,
+                                       C.c_void_p(full.data_ptr()), C.c_void_p(stream.cuda_stream))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms, rng_ms, rays_local = [], [], 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(st.ms_kernel)
+        rng_ms.append(st.ms_rng)
+        rays_local += st.rays_intersect + st.rays_occluded
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays_local], dtype=torch.float64, device=dev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_total = float(r.item())
+    else:
+        rays_total = float(rays_local)
+
+    # Instrumented pass (outside the timed region) for the FLOP model.
+    st_ops = rtamd.Stats()
+    step(flags | rtamd.RT_FLAG_COUNT_OPS, st_ops)
+    torch.cuda.synchronize()
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 0
+
+    ops = {rtamd.OP_NAMES[i]: int(st_ops.ops[i]) for i in range(16)}
+    ops["_occluded"] = int(st_ops.rays_occluded)
+    primary = n_rows * W * (1 if mode == 1 else 8)
+    flops, transc = model_flops(ops, primary, mode == 1)
+    k_ms = sum(kernel_ms) / len(kernel_ms)
+    achieved = flops / (k_ms * 1e-3) / 1e12
+    value = rays_total / elapsed / 1e6
+    rays_per_frame = rays_total / args.steps
+
+    prof_traffic = None
+    tpath = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        try:
+            with open(tpath) as f:
+                tj = json.load(f)
+            if tj.get("config") == args.config and world == 1:
+                prof_traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            prof_traffic = None
+
+    cpu = None
+    if not args.no_cpu and world == 1:
+        # bounded sample: a band of rows from the middle of the same frame,
+        # single-threaded CPU oracle (C port of the reference path)
+        r0 = max(0, H // 2 - args.cpu_rows // 2)
+        r1 = min(H, r0 + args.cpu_rows)
+        tc = time.perf_counter()
+        _, ost = rtamd.oracle_render(sc, W, H, mode, r0, r1, threads=1)
+        dt = time.perf_counter() - tc
+        cpu_rays = ost.rays_intersect + ost.rays_occluded
+        cpu = {"value": round(cpu_rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
+               "sample": f"config {args.config} output rows [{r0},{r1}) x {W} px, {cpu_rays} rays in {dt:.1f} s "
+                         f"on {platform.processor() or platform.machine()} (oracle/oracle.c, 1 thread)"}
+
+    name = scenes.CONFIGS[args.config][0]
+    out = {
+        "metric": "Mrays/s (primary+secondary) + wall-clock per frame, 4K scene @1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: reference example scene JSON + mt19937(12345) jitter, rendered on device",
+        "config": {"workload": name, "width": W, "height": H, "mode": "paper" if mode else "standard",
+                   "rays_per_frame": int(rays_per_frame), "parallelism": f"row-strips{STRIP}x{world}",
+                   "cull": not args.no_cull},
+        "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
+                     "traffic": prof_traffic, "kernel": "k_std" if mode == 0 else "k_paper_primary",
+                     "kernel_ms": round(k_ms, 3), "flops_per_launch": flops, "transcendentals": transc,
+                     "hbm_frac": None if prof_traffic is None else
+                     round(prof_traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
+        "rng_ms": round(sum(rng_ms) / len(rng_ms), 3),
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

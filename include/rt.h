@@ -185,8 +185,8 @@ enum rt_op_counter {
     RT_OPC_SHADE_SPEC,          /* ... with a specular pow()               */
     RT_OPC_SECONDARY,           /* reflection/refraction spawns            */
     RT_OPC_CULLED,              /* subtree evaluations skipped by a wave-uniform bound cull */
-    RT_OPC_RESERVED0,
-    RT_OPC_RESERVED1
+    RT_OPC_LIGHT_EVAL,          /* point-light loop iterations in shading  */
+    RT_OPC_SHADE_CALL           /* shade_lambert_phong calls with a material */
 };
 
 enum rt_flags {

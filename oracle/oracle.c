@@ -470,12 +470,14 @@ static inline V3 combine(V3 a, V3 b) {
 static V3 shade(Ctx* c, const Hit* hit, V3 wo) {
     if (hit->mat < 0) return v3(1, 0, 1);
     const rt_scene_desc* s = c->s;
+    c->st.ops[RT_OPC_SHADE_CALL]++;
     const rt_material* m = &s->materials[hit->mat];
     const V3 n = hit->n;
     V3 E_total = v3(m->ambient[0] * s->ambient[0], m->ambient[1] * s->ambient[1], m->ambient[2] * s->ambient[2]);
     const double shadow_epsilon = dmax(1e-3, 1e-4 * hit->t);
     for (int li = 0; li < s->n_lights; ++li) {
         const rt_light* L = &s->lights[li];
+        c->st.ops[RT_OPC_LIGHT_EVAL]++;
         V3 to_light = v3(L->pos[0] - hit->p.x, L->pos[1] - hit->p.y, L->pos[2] - hit->p.z);
         double dist_squared = dot3(to_light, to_light);
         if (dist_squared <= 0.01) dist_squared = 0.01;

@@ -481,8 +481,8 @@ struct IStack {
 };
 
 // Evaluate one OBJ_PROG object: Primitive::intersect(root, ray, tmin, tmax).
-template <class CT>
-__device__ __noinline__ bool run_program(const DevScene& S, int pc0, int pc1, const DRay& world, double tmin,
+template <bool EAGER, class CT>
+__device__ __forceinline__ bool run_program(const DevScene& S, int pc0, int pc1, const DRay& world, double tmin,
                                          double tmax, double& t_out, DHit& h_out, CT& cnt) {
     DRay cur = world;
     DRay rstk[kMaxRayStack];
@@ -578,6 +578,385 @@ __device__ __noinline__ bool run_program(const DevScene& S, int pc0, int pc1, co
     return hit.ok;
 }
 
+// ================================================================ compact
+// Lazy hit references (DESIGN.md §Lazy hits).  An interval endpoint in a
+// compact CSG program is (t_ref, code): code = op index of the leaf | ROOT1
+// (exit root) | FLIP (a CSG difference re-faced it: csg.cpp:140-150 leaves n
+// unchanged and sets front_face=false) | ORIGIN (the inside-at-origin entry of
+// csg.cpp:113-122: p = ray.o, n = 0, material of the referenced leaf hit).
+// The normal / material of a referenced hit is a pure function of (frame
+// ray, leaf, t_ref), so it is recomputed bit-identically only for the hit
+// that wins.
+constexpr int REF_PC_MASK = (1 << 22) - 1;
+constexpr int REF_ROOT1 = 1 << 22;
+constexpr int REF_FLIP = 1 << 23;
+constexpr int REF_ORIGIN = 1 << 24;
+
+struct CIvl {
+    int ok;
+    double t0, t1;   // interval (event times)
+    double s0, s1;   // t_ref of the entry / exit hit references
+    int c0, c1;      // codes of the entry / exit hit references
+};
+
+// Primitive::interval for a leaf without computing hit points or normals
+// (geometry.cpp:48-78, 117-147, 207-217).
+template <class CT>
+__device__ __forceinline__ void leaf_ivl_c(const rt_node* nd, int pc, const DRay& r, CIvl& o, CT& cnt) {
+    o.c0 = pc;
+    o.c1 = pc | REF_ROOT1;
+    if (nd->kind == RT_NODE_HALFSPACE) {
+        cnt.inc(RT_OPC_HALF_IVL);
+        const V3 n = ld3(nd->v + 3);
+        const double ndotd = dot3(n, r.d);
+        V3 diff = v3(r.o.x - nd->v[0], r.o.y - nd->v[1], r.o.z - nd->v[2]);
+        const double f0 = dot3(n, diff);
+        if (__builtin_fabs(ndotd) < 1e-12) {
+            o.ok = f0 >= 0.0;
+            o.t0 = -RT_INF;
+            o.t1 = RT_INF;
+        } else {
+            o.ok = 1;
+            const double tPlane = -f0 / ndotd;
+            o.t0 = ndotd > 0.0 ? tPlane : -RT_INF;
+            o.t1 = ndotd > 0.0 ? RT_INF : tPlane;
+        }
+    } else {
+        cnt.inc(RT_OPC_SPHERE_IVL);
+        const double r0 = nd->v[3];
+        V3 oc = v3(r.o.x - nd->v[0], r.o.y - nd->v[1], r.o.z - nd->v[2]);
+        const double half_b = dot3(oc, r.d);
+        const double cterm = dot3(oc, oc) - r0 * r0;
+        const double disc = half_b * half_b - 1.0 * cterm;
+        o.ok = !(disc < 0.0);
+        const double s = __builtin_sqrt(o.ok ? disc : 0.0);
+        double t0 = (-half_b - s) / 1.0;
+        double t1 = (-half_b + s) / 1.0;
+        if (t0 > t1) {
+            const double tt = t0;
+            t0 = t1;
+            t1 = tt;
+        }
+        o.t0 = t0;
+        o.t1 = t1;
+        if (o.ok) cnt.inc(RT_OPC_SPHERE_IVL_HIT);
+    }
+    o.s0 = o.t0;
+    o.s1 = o.t1;
+}
+
+// CSG::interval (csg.cpp:61-163) on two compact child intervals.
+template <class CT>
+__device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl& R, CT& cnt) {
+    R.ok = 0;
+    R.t0 = R.t1 = R.s0 = R.s1 = 0.0;
+    R.c0 = R.c1 = 0;
+    if (!A.ok && !B.ok) return;
+    cnt.inc(RT_OPC_CSG_COMBINE);
+    // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
+    double et[4];
+    int ec[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        et[k] = 0.0;
+        ec[k] = 0;
+    }
+    int n = 0;
+    {
+        const double tv[4] = {A.t0, A.t1, B.t0, B.t1};
+        const bool pv[4] = {A.ok && __builtin_isfinite(A.t0), A.ok && __builtin_isfinite(A.t1),
+                            B.ok && __builtin_isfinite(B.t0), B.ok && __builtin_isfinite(B.t1)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool here = pv[e] && n == k;
+                et[k] = here ? tv[e] : et[k];
+                ec[k] = here ? e : ec[k];
+            }
+            n += pv[e] ? 1 : 0;
+        }
+    }
+    // libstdc++ __insertion_sort (stl_algo.h:1819-1871) with the non-strict
+    // comparator, unrolled over the fixed <= 4 slots.
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        if (i < n) {
+            const double vt = et[i];
+            const int vc = ec[i];
+            if (ev_less(vt, vc, et[0], ec[0])) {
+#pragma unroll
+                for (int k = i; k > 0; --k) {
+                    et[k] = et[k - 1];
+                    ec[k] = ec[k - 1];
+                }
+                et[0] = vt;
+                ec[0] = vc;
+            } else {
+                bool moving = true;
+                int last = i;
+#pragma unroll
+                for (int k = i; k > 0; --k) {
+                    if (moving && ev_less(vt, vc, et[k - 1], ec[k - 1])) {
+                        et[k] = et[k - 1];
+                        ec[k] = ec[k - 1];
+                        last = k - 1;
+                    } else {
+                        moving = false;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k == last) {
+                        et[k] = vt;
+                        ec[k] = vc;
+                    }
+            }
+        }
+    }
+    bool inA = A.ok && (A.t0 < 1e-6) && (A.t1 > 1e-6);
+    bool inB = B.ok && (B.t0 < 1e-6) && (B.t1 > 1e-6);
+    bool inR = csg_combine(op, inA, inB);
+    const bool origin = inR;
+    bool haveEnter = inR;
+    int enterE = -1, exitE = -1;
+    bool flipE = false, flipX = false;
+    double tEnt = 0.0, tExt = RT_INF;
+    const bool originFromA = inA;
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < n && !done) {
+            const bool before = inR;
+            const int e = ec[k];
+            const bool enter = (e & 1) == 0;
+            if ((e >> 1) == 0) inA = enter;
+            else inB = enter;
+            const bool after = csg_combine(op, inA, inB);
+            if (!before && after) {
+                haveEnter = true;
+                tEnt = et[k];
+                enterE = e;
+                flipE = (op == RT_CSG_DIFFERENCE) && e == 3;
+            } else if (before && !after) {
+                tExt = et[k];
+                exitE = e;
+                flipX = (op == RT_CSG_DIFFERENCE) && e == 2;
+                done = true;
+            }
+            if (!done) inR = after;
+        }
+    }
+    if (!haveEnter || !__builtin_isfinite(tExt)) return;
+    R.ok = 1;
+    R.t0 = tEnt;
+    R.t1 = tExt;
+    if (enterE < 0) {
+        // origin hit: material source = A.h0 if inside A else B.h0 (leaf materials are never null here)
+        (void)origin;
+        R.s0 = originFromA ? A.s0 : B.s0;
+        R.c0 = ((originFromA ? A.c0 : B.c0) & ~REF_FLIP) | REF_ORIGIN;
+    } else {
+        R.s0 = enterE == 0 ? A.s0 : enterE == 1 ? A.s1 : enterE == 2 ? B.s0 : B.s1;
+        R.c0 = (enterE == 0 ? A.c0 : enterE == 1 ? A.c1 : enterE == 2 ? B.c0 : B.c1) | (flipE ? REF_FLIP : 0);
+    }
+    R.s1 = exitE == 0 ? A.s0 : exitE == 1 ? A.s1 : exitE == 2 ? B.s0 : B.s1;
+    R.c1 = (exitE == 0 ? A.c0 : exitE == 1 ? A.c1 : exitE == 2 ? B.c0 : B.c1) | (flipX ? REF_FLIP : 0);
+}
+
+struct CStack {
+    CIvl tos, nos;
+    CIvl spill[kMaxIvlSpill];
+    int sp;   // entries (wave-uniform)
+    __device__ __forceinline__ void push(const CIvl& v) {
+        if (sp >= 2) spill[sp - 2] = nos;
+        if (sp >= 1) nos = tos;
+        tos = v;
+        ++sp;
+    }
+    __device__ __forceinline__ void reduce2(const CIvl& r) {
+        tos = r;
+        if (sp >= 3) nos = spill[sp - 3];
+        --sp;
+    }
+};
+
+// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
+template <class CT>
+__device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1, const DRay& r, CT& cnt) {
+    CStack st;
+    st.sp = 0;
+    for (int pc = pc0; pc < pc1; ++pc) {
+        const DevOp op = S.ops[pc];
+        if (op.op == rtamd::OP_LEAF_IVL) {
+            CIvl v;
+            leaf_ivl_c(&S.nodes[op.node], pc, r, v, cnt);
+            st.push(v);
+        } else {
+            CIvl v;
+            csg_c(op.csg_op, st.nos, st.tos, v, cnt);
+            st.reduce2(v);
+        }
+    }
+    return st.tos;
+}
+
+// Leaf Primitive::intersect without normal (t and acceptance only).
+template <class CT>
+__device__ __forceinline__ bool leaf_hit_t(const rt_node* nd, const DRay& r, double tmin, double tmax, double& t,
+                                           CT& cnt) {
+    if (nd->kind == RT_NODE_HALFSPACE) {   // geometry.cpp:90-106
+        cnt.inc(RT_OPC_HALF_ISECT);
+        const V3 n = ld3(nd->v + 3);
+        const double ndotd = dot3(n, r.d);
+        if (__builtin_fabs(ndotd) < 1e-12) return false;
+        V3 diff = v3(nd->v[0] - r.o.x, nd->v[1] - r.o.y, nd->v[2] - r.o.z);
+        t = dot3(n, diff) / ndotd;
+        const bool ok = !(t < tmin || t > tmax);
+        if (ok) cnt.inc(RT_OPC_HALF_ISECT_HIT);
+        return ok;
+    }
+    cnt.inc(RT_OPC_SPHERE_ISECT);   // geometry.cpp:12-37
+    const double rad = nd->v[3];
+    V3 oc = v3(r.o.x - nd->v[0], r.o.y - nd->v[1], r.o.z - nd->v[2]);
+    const double half_b = dot3(oc, r.d);
+    const double cterm = dot3(oc, oc) - rad * rad;
+    const double disc = half_b * half_b - 1.0 * cterm;
+    if (disc < 0.0) return false;
+    const double sq = __builtin_sqrt(disc);
+    t = (-half_b - sq) / 1.0;
+    if (t < tmin || t > tmax) {
+        t = (-half_b + sq) / 1.0;
+        if (t < tmin || t > tmax) return false;
+    }
+    cnt.inc(RT_OPC_SPHERE_ISECT_HIT);
+    return true;
+}
+
+// Normal / front_face / material of a leaf hit at point p on frame ray r.
+template <class CT>
+__device__ __forceinline__ void leaf_shading(const rt_node* nd, const DRay& r, V3 p, DHit& h, CT& cnt) {
+    if (nd->kind == RT_NODE_HALFSPACE) {
+        set_face_normal(h, r, ld3(nd->v + 3));
+        h.mat = nd->mat;
+        return;
+    }
+    const double rad = nd->v[3];
+    const V3 outward = v3((p.x - nd->v[0]) / rad, (p.y - nd->v[1]) / rad, (p.z - nd->v[2]) / rad);
+    set_face_normal(h, r, outward);
+    h.mat = nd->kind == RT_NODE_SPHERE ? nd->mat : pick_region(nd, p, cnt);
+}
+
+// Resolve a compact hit reference on frame ray r into (n, ff, mat).
+template <class CT>
+__device__ __forceinline__ void resolve_ref(const DevScene& S, const DRay& r, double ts, int code, DHit& h,
+                                            CT& cnt) {
+    const rt_node* nd = &S.nodes[S.ops[code & REF_PC_MASK].node];
+    const V3 p = __builtin_isfinite(ts) ? ray_at(r, ts) : r.o;
+    leaf_shading(nd, r, p, h, cnt);
+    if (code & REF_ORIGIN) {
+        h.n = v3(0.0, 0.0, 0.0);
+        h.ff = 1;
+    }
+    if (code & REF_FLIP) h.ff = 0;
+}
+
+// Ray at depth k of an object's transform chain (k = 0: world).
+__device__ __forceinline__ DRay chain_ray(const DevScene& S, int pc0, int k, const DRay& world) {
+    DRay r = world;
+    for (int i = 0; i < k; ++i) r = local_ray(&S.nodes[S.ops[pc0 + i].node], r);
+    return r;
+}
+
+
+// Primitive::intersect(object, ray, tmin, tmax): hit t, hit point p and a lazy
+// reference (ts, code) resolved later by resolve_hit().
+template <bool EAGER, class CT>
+__device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, const DRay& world, double tmin,
+                                           double tmax, double& t, V3& p, double& ts, int& code, CT& cnt) {
+    if (ob.kind <= rtamd::OBJ_POKE) {
+        const bool ok = leaf_hit_t(&S.nodes[ob.node], world, tmin, tmax, t, cnt);
+        p = ray_at(world, t);
+        ts = t;
+        code = 0;
+        return ok;
+    }
+    if (ob.kind == rtamd::OBJ_CHAIN) {
+        // transforms (transform.cpp): local ray, child on [0,inf), map back, project t
+        DRay cur = world;
+        for (int k = 0; k < ob.m; ++k) {
+            cnt.inc(RT_OPC_XFORM);
+            cur = local_ray(&S.nodes[S.ops[ob.pc0 + k].node], cur);
+        }
+        const double lo = ob.m ? 0.0 : tmin;
+        const double hi = ob.m ? RT_INF : tmax;
+        bool ok;
+        if (ob.core == 0) {
+            ok = leaf_hit_t(&S.nodes[ob.node], cur, lo, hi, t, cnt);
+            p = ray_at(cur, t);
+            ts = t;
+            code = ob.cpc0;
+        } else {   // CSG::intersect (csg.cpp:169-185)
+            const CIvl R = run_compact(S, ob.cpc0, ob.cpc1, cur, cnt);
+            t = dmax(R.t0, lo);
+            ok = R.ok && (t < R.t1 && t < hi);
+            p = v3(cur.o.x + cur.d.x * t, cur.o.y + cur.d.y * t, cur.o.z + cur.d.z * t);
+            ts = R.s0;
+            code = R.c0;
+        }
+        for (int k = ob.m - 1; k >= 0; --k) {
+            const DRay parent = (k == 0) ? world : chain_ray(S, ob.pc0, k, world);
+            const rt_node* nd = &S.nodes[S.ops[ob.pc0 + k].node];
+            const V3 wp = map_point(nd, p);
+            const double wt = project_t_world(parent, wp);
+            const double l = k ? 0.0 : tmin, h = k ? RT_INF : tmax;
+            ok = ok && (wt > l && wt < h);
+            p = wp;
+            t = wt;
+        }
+        return ok;
+    }
+    if constexpr (EAGER) {
+        if (ob.kind == rtamd::OBJ_EAGER) {
+            DHit h;
+            const bool ok = run_program<EAGER>(S, ob.pc0, ob.pc1, world, tmin, tmax, t, h, cnt);
+            p = h.p;
+            ts = t;
+            code = 0;
+            return ok;
+        }
+    }
+    return false;
+}
+
+// Full hit record (p, n, front_face, mat) of the winning object.
+template <bool EAGER, class CT>
+__device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DRay& world, double tmin, V3 p,
+                                            double ts, int code, DHit& h, CT& cnt) {
+    const DevObj ob = S.objs[obj];
+    h.p = p;
+    if (ob.kind <= rtamd::OBJ_POKE) {
+        leaf_shading(&S.nodes[ob.node], world, p, h, cnt);
+        return;
+    }
+    if (ob.kind == rtamd::OBJ_CHAIN) {
+        const DRay cur = chain_ray(S, ob.pc0, ob.m, world);
+        if (ob.core == 0) leaf_shading(&S.nodes[ob.node], cur, ray_at(cur, ts), h, cnt);
+        else resolve_ref(S, cur, ts, code, h, cnt);
+        for (int k = ob.m - 1; k >= 0; --k) {   // normals back through the chain
+            const DRay parent = (k == 0) ? world : chain_ray(S, ob.pc0, k, world);
+            const V3 wn = map_normal(&S.nodes[S.ops[ob.pc0 + k].node], h.n);
+            set_face_normal(h, parent, wn);
+        }
+        return;
+    }
+    if constexpr (EAGER) {   // re-run the eager program (result does not depend on tmax)
+        double t;
+        run_program<EAGER>(S, ob.pc0, ob.pc1, world, tmin, RT_INF, t, h, cnt);
+        h.p = p;
+    }
+}
+
 // Conservative test: can the ray's [tmin,tmax] segment touch the bound?
 __device__ __forceinline__ bool bound_touch(const DevObj& ob, const DRay& r, double tmin, double tmax) {
     V3 oc = v3(r.o.x - ob.bc[0], r.o.y - ob.bc[1], r.o.z - ob.bc[2]);
@@ -592,62 +971,62 @@ __device__ __forceinline__ bool bound_touch(const DevObj& ob, const DRay& r, dou
     return !(t1 < tmin - m0) && !(t0 > tmax + m1);
 }
 
-// Primitive::intersect for top-level object o (Scene::intersect body, scene.cpp:18).
-template <class CT>
-__device__ __forceinline__ bool object_intersect(const DevScene& S, const DevObj& ob, const DRay& r, double tmin,
-                                                 double tmax, double& t, DHit& h, CT& cnt) {
-    if (ob.kind == rtamd::OBJ_PROG) return run_program(S, ob.pc0, ob.pc1, r, tmin, tmax, t, h, cnt);
-    return leaf_intersect(&S.nodes[ob.node], r, tmin, tmax, t, h, cnt);
-}
-
-// Scene::intersect (scene.cpp:10-24): closest hit, later objects win ties
-// exactly as in the reference (each object applies its own accept rule).
-template <class CT>
+// Scene::intersect (scene.cpp:10-24): closest hit; every object applies its
+// own accept rule with tmax = closest-so-far, so ties resolve as in the
+// reference (Sphere/HalfSpace accept t == tmax, CSG/transforms do not).
+template <bool EAGER, class CT>
 __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, double tmax, double& t_best,
                                 DHit& best, CT& cnt) {
-    bool any = false;
     double closest = tmax;
+    int win = -1;
+    V3 wp = v3(0.0, 0.0, 0.0);
+    double wts = 0.0;
+    int wcode = 0;
     for (int o = 0; o < S.n_objs; ++o) {
         const DevObj ob = S.objs[o];
         if (ob.kind == rtamd::OBJ_NEVER) continue;
-        if (ob.kind == rtamd::OBJ_PROG && ob.has_bound && S.cull) {
-            const bool need = bound_touch(ob, r, tmin, closest);
-            if (!__any(need)) {
+        if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound && S.cull) {
+            if (!__any(bound_touch(ob, r, tmin, closest))) {
                 cnt.inc(RT_OPC_CULLED);
                 continue;
             }
         }
-        double t;
-        DHit h;
-        if (object_intersect(S, ob, r, tmin, closest, t, h, cnt)) {
-            any = true;
+        double t = 0.0, ts = 0.0;
+        V3 p;
+        int code = 0;
+        if (object_hit<EAGER>(S, ob, r, tmin, closest, t, p, ts, code, cnt)) {
             closest = t;
-            best = h;
-            t_best = t;
+            win = o;
+            wp = p;
+            wts = ts;
+            wcode = code;
         }
     }
-    return any;
+    if (win < 0) return false;
+    resolve_hit<EAGER>(S, win, r, tmin, wp, wts, wcode, best, cnt);
+    t_best = closest;
+    return true;
 }
 
 // Scene::occluded (scene.cpp:33-42): any hit; per-lane early exit.
-template <class CT>
+template <bool EAGER, class CT>
 __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, double tmax, CT& cnt) {
     bool hit = false;
     for (int o = 0; o < S.n_objs; ++o) {
         if (__all(hit)) break;
         const DevObj ob = S.objs[o];
         if (ob.kind == rtamd::OBJ_NEVER) continue;
-        if (ob.kind == rtamd::OBJ_PROG && ob.has_bound && S.cull) {
-            const bool need = !hit && bound_touch(ob, r, tmin, tmax);
-            if (!__any(need)) {
+        if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound && S.cull) {
+            if (!__any(!hit && bound_touch(ob, r, tmin, tmax))) {
                 cnt.inc(RT_OPC_CULLED);
                 continue;
             }
         }
         if (!hit) {
-            double t;
-            DHit h;
-            hit = object_intersect(S, ob, r, tmin, tmax, t, h, cnt);
+            double t = 0.0, ts = 0.0;
+            V3 p;
+            int code = 0;
+            hit = object_hit<EAGER>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
         }
     }
     return hit;
@@ -660,9 +1039,10 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 
 // shade_lambert_phong (shading.cpp:31-138), point lights only (the loader
 // never populates directional lights).
-template <class CT>
+template <bool EAGER, class CT>
 __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
     if (hit.mat < 0) return v3(1.0, 0.0, 1.0);
+    cnt.inc(RT_OPC_SHADE_CALL);
     const rt_material* m = &S.mats[hit.mat];
     const V3 n = hit.n;
     V3 E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
@@ -671,6 +1051,7 @@ __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32
     const V3 alb = ld3(m->albedo);
     for (int li = 0; li < S.n_lights; ++li) {
         const rt_light* L = &S.lights[li];
+        cnt.inc(RT_OPC_LIGHT_EVAL);
         V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
         double d2 = dot3(tl, tl);
         if (d2 <= 0.01) d2 = 0.01;
@@ -683,7 +1064,7 @@ __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32
         const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
         const DRay sr = make_ray(so, wi);
         ++n_occl;
-        if (scene_occluded(S, sr, eps, max_t, cnt)) continue;
+        if (scene_occluded<EAGER>(S, sr, eps, max_t, cnt)) continue;
         cnt.inc(RT_OPC_SHADE_LIGHT);
         const double ed = dmax(0.5, dist);
         const double falloff = 1.0 / (ed * ed);
@@ -718,8 +1099,18 @@ struct Frame {
 };
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
-template <class CT>
+template <bool EAGER, bool SECONDARY, class CT>
 __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+    if constexpr (!SECONDARY) {
+        // No material reflects or refracts (or recursion <= 1): trace_recursive
+        // reduces to one closest hit + local shading (tracer.cpp:22-37, 72).
+        if (S.rec_limit <= 0) return v3(0.0, 0.0, 0.0);
+        double ht = 0.0;
+        DHit h;
+        ++n_isect;
+        if (!scene_intersect<EAGER>(S, r, 1e-4, RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+        return shade<EAGER>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
+    }
     Frame stk[kMaxDepth];
     int sp = 0;
     int depth = 0;
@@ -734,11 +1125,11 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
             double ht = 0.0;
             DHit h;
             ++n_isect;
-            if (!scene_intersect(S, r, 1e-4, RT_INF, ht, h, cnt)) {
+            if (!scene_intersect<EAGER>(S, r, 1e-4, RT_INF, ht, h, cnt)) {
                 ret = v3(S.bg[0], S.bg[1], S.bg[2]);
             } else {
                 const V3 wo = normalized(vneg(r.d));
-                const V3 direct = shade(S, ht, h, wo, n_occl, cnt);
+                const V3 direct = shade<EAGER>(S, ht, h, wo, n_occl, cnt);
                 if (h.mat < 0) {
                     ret = direct;
                 } else {

@@ -169,26 +169,87 @@ public:
         throw std::runtime_error("unknown node kind");
     }
 
+    // CSG subtree made of CSG nodes and leaves only, every leaf with a material.
+    bool compact_csg(int idx, int level) {
+        if (level > 4096) throw std::runtime_error("scene graph too deep");
+        const rt_node& n = d_.nodes[idx];
+        switch (n.kind) {
+            case RT_NODE_SPHERE:
+            case RT_NODE_HALFSPACE:
+                return n.mat >= 0;
+            case RT_NODE_POKEBALL:
+                for (int k = 0; k < 5; ++k)
+                    if (n.mats[k] < 0) return false;
+                return true;
+            case RT_NODE_CSG:
+                return compact_csg(n.a, level + 1) && compact_csg(n.b, level + 1);
+            default:
+                return false;
+        }
+    }
+
+    void emit_compact_ivl(int idx) {
+        const rt_node& n = d_.nodes[idx];
+        if (n.kind == RT_NODE_CSG) {
+            emit_compact_ivl(n.a);
+            emit_compact_ivl(n.b);
+            DevOp& o = op(OP_CSG, idx, 0);
+            o.csg_op = n.op;
+            --idepth_;
+            return;
+        }
+        op(OP_LEAF_IVL, idx, 0);
+        ivl_push();
+    }
+
     CompiledScene run() {
         CompiledScene cs;
         ops_ = &cs.ops;
+        for (int k = 0; k < d_.n_nodes; ++k)
+            if (d_.nodes[k].kind == RT_NODE_POKEBALL) cs.has_pokeball = true;
         for (int i = 0; i < d_.n_objects; ++i) {
             int idx = d_.objects[i];
-            const rt_node& n = d_.nodes[idx];
             DevObj o{};
             o.node = idx;
+            o.pc0 = o.pc1 = o.cpc0 = o.cpc1 = (int)cs.ops.size();
             Bound b = bound(idx);
-            if (b.kind == Bound::Empty) {
+            // transform chain above the core
+            std::vector<int> chain;
+            int core = idx;
+            bool degenerate = false;
+            while (d_.nodes[core].kind >= RT_NODE_TRANSLATION && d_.nodes[core].kind <= RT_NODE_ROTATION) {
+                if (is_degenerate_scaling(d_.nodes[core])) degenerate = true;
+                chain.push_back(core);
+                core = d_.nodes[core].a;
+            }
+            const rt_node& cn = d_.nodes[core];
+            const bool leaf_core = cn.kind == RT_NODE_SPHERE || cn.kind == RT_NODE_HALFSPACE || cn.kind == RT_NODE_POKEBALL;
+            if (b.kind == Bound::Empty || degenerate) {
                 o.kind = OBJ_NEVER;
-            } else if (n.kind == RT_NODE_SPHERE) {
-                o.kind = OBJ_SPHERE;
-            } else if (n.kind == RT_NODE_HALFSPACE) {
-                o.kind = OBJ_HALF;
-            } else if (n.kind == RT_NODE_POKEBALL) {
-                o.kind = OBJ_POKE;
+            } else if (chain.empty() && leaf_core) {
+                o.kind = cn.kind == RT_NODE_SPHERE ? OBJ_SPHERE : cn.kind == RT_NODE_HALFSPACE ? OBJ_HALF : OBJ_POKE;
+            } else if (leaf_core || (cn.kind == RT_NODE_CSG && compact_csg(core, 0))) {
+                o.kind = OBJ_CHAIN;
+                o.m = (int)chain.size();
+                rdepth_ = idepth_ = 0;
+                for (int t : chain) {
+                    op(OP_XPUSH, t, 0);
+                    ray_push();
+                }
+                o.node = core;
+                o.cpc0 = (int)cs.ops.size();
+                if (leaf_core) {
+                    o.core = 0;
+                    op(OP_LEAF_ISECT, core, 0);
+                } else {
+                    o.core = 1;
+                    emit_compact_ivl(core);
+                }
+                o.cpc1 = (int)cs.ops.size();
+                o.pc1 = o.cpc1;
             } else {
-                o.kind = OBJ_PROG;
-                o.strict = 1;
+                o.kind = OBJ_EAGER;
+                cs.has_eager = true;
                 o.pc0 = (int)cs.ops.size();
                 rdepth_ = idepth_ = 0;
                 emit_isect(idx, 1, 0);

@@ -1,12 +1,18 @@
 // scene_compile.hpp — lowers the scene IR (include/rt.h) to the device form.
 //
-// Every top-level object becomes one DevObj.  Leaf primitives are evaluated
-// directly; any object involving a transform or a CSG node becomes a short
-// post-order program of DevOps that the device interprets with WAVE-UNIFORM
-// control flow (every lane runs the same op sequence; only data differs),
+// Every top-level object becomes one DevObj, evaluated with WAVE-UNIFORM
+// control flow (every lane walks the same op sequence; only data differs),
 // replacing the reference's virtual recursion (Primitive::intersect /
-// ::interval, geometry.h:62-75) with an explicit ray stack (transforms) and
-// interval stack (CSG operands).
+// ::interval, geometry.h:62-75):
+//   OBJ_SPHERE / OBJ_HALF / OBJ_POKE  a bare leaf primitive,
+//   OBJ_CHAIN  a chain of m >= 0 transforms over either one leaf or a CSG tree
+//              whose operands are leaves / CSG nodes only.  Intervals carry
+//              lazy hit references; normals and materials are resolved once
+//              for the winning hit (DESIGN.md §Lazy hits),
+//   OBJ_EAGER  anything else (a transform inside a CSG operand): a general
+//              post-order program with full hit records (rare; its own
+//              kernel variant so it never costs the common case registers),
+//   OBJ_NEVER  can never report a hit (degenerate Scaling, transform.cpp:97).
 #pragma once
 
 #include <cstdint>
@@ -17,26 +23,36 @@
 
 namespace rtamd {
 
-enum DevObjKind : int32_t { OBJ_SPHERE = 0, OBJ_HALF = 1, OBJ_POKE = 2, OBJ_PROG = 3, OBJ_NEVER = 4 };
+enum DevObjKind : int32_t {
+    OBJ_SPHERE = 0,
+    OBJ_HALF = 1,
+    OBJ_POKE = 2,
+    OBJ_CHAIN = 3,
+    OBJ_EAGER = 4,
+    OBJ_NEVER = 5
+};
 
 enum DevOpCode : int32_t {
     OP_XPUSH = 0,       // push current ray, current = local ray of transform node
     OP_LEAF_IVL = 1,    // push Primitive::interval(leaf, current ray)
     OP_CSG = 2,         // pop b, pop a, push CSG::interval combine(op)
-    OP_XPOP_IVL = 3,    // map top interval back through transform node, pop ray
+    OP_XPOP_IVL = 3,    // (eager) map top interval back through transform node, pop ray
     OP_LEAF_ISECT = 4,  // hit = Primitive::intersect(leaf, current ray, range)
     OP_CSG_ISECT = 5,   // hit = CSG::intersect from top interval, range
-    OP_XPOP_HIT = 6,    // map hit back through transform node, check range, pop ray
+    OP_XPOP_HIT = 6,    // (eager) map hit back through transform node, check range, pop ray
     OP_NEVER = 7        // the subtree can never hit (degenerate Scaling, transform.cpp:97)
 };
 
 struct DevObj {
     int32_t kind;
-    int32_t node;       // IR node index (leaf kinds)
-    int32_t pc0, pc1;   // program range (OBJ_PROG)
+    int32_t node;       // leaf node (bare leaves; CHAIN with a leaf core)
+    int32_t pc0;        // CHAIN: first XPUSH op; EAGER: program start
+    int32_t m;          // CHAIN: number of transforms in the chain
+    int32_t core;       // CHAIN: 0 = leaf core, 1 = CSG core
+    int32_t cpc0, cpc1; // CHAIN: leaf core -> cpc0 = its LEAF_ISECT op; CSG core -> [cpc0,cpc1) compact program
+    int32_t pc1;        // EAGER: program end
     int32_t has_bound;  // conservative world-space bounding sphere present
-    int32_t strict;     // 1 = accepts only t < tmax (CSG / transforms), 0 = t <= tmax
-    int32_t pad[2];
+    int32_t pad;
     double bc[3];       // bound centre
     double br;          // bound radius (already inflated)
 };
@@ -44,7 +60,7 @@ struct DevObj {
 struct DevOp {
     int32_t op;
     int32_t node;       // IR node index (leaf / transform / csg)
-    int32_t top;        // 1 = range is the query's (tmin,tmax); 0 = nested (0,inf)
+    int32_t top;        // eager: 1 = range is the query's (tmin,tmax); 0 = nested (0,inf); 2 = NEVER in interval mode
     int32_t csg_op;
 };
 
@@ -53,6 +69,8 @@ struct CompiledScene {
     std::vector<DevOp> ops;
     int max_ray_depth = 0;   // transform nesting on any path
     int max_ivl_depth = 0;   // interval stack depth on any path
+    bool has_eager = false;  // some object needs the eager interpreter
+    bool has_pokeball = false;
 };
 
 // Throws std::runtime_error on malformed IR.

@@ -42,7 +42,7 @@ CSG_UNION, CSG_INTERSECTION, CSG_DIFFERENCE = range(3)
 OP_NAMES = [
     "sphere_isect", "sphere_isect_hit", "sphere_ivl", "sphere_ivl_hit", "half_isect", "half_isect_hit",
     "half_ivl", "poke_region", "csg_combine", "xform", "shade_light", "shade_spec", "secondary", "culled",
-    "reserved0", "reserved1",
+    "light_eval", "shade_call",
 ]
 
 

@@ -216,6 +216,22 @@ def torture_scenes(dpi: int = 24) -> dict[str, dict]:
                         "color": _mat([0.5, 0.5, 0.8], refracted=[0.6, 0.6, 0.6], reflected=[0.3, 0.3, 0.3])}},
             {"sphere": {"position": [0.0, 1.0, -2.5], "radius": 0.3, "color": _mat([0.9, 0.2, 0.2])}}]},
     ], recursion=6, dpi=dpi)
+    t_sph = {"translation": {"factors": [-1.2, 0.2, -1.0], "subject": {
+        "sphere": {"position": [0, 0, 0], "radius": 0.6, "color": _mat([0.8, 0.3, 0.3])}}}}
+    r_sph = {"rotation": {"angle": 35, "direction": 2, "subject": {"scaling": {"factors": [1.6, 0.5, 0.8], "subject": {
+        "sphere": {"position": [-0.5, 0, -1.2], "radius": 0.5, "color": _mat([0.3, 0.8, 0.3])}}}}}}
+    t_half = {"translation": {"factors": [0.0, 0.3, 0.0], "subject": {
+        "halfSpace": {"position": [1.3, 0.0, -1.0], "normal": [0, 1, 0.2], "color": _mat([0.9, 0.9, 0.9])}}}}
+    s_poke = {"scaling": {"factors": [1.0, 2.0, 1.0], "subject": {
+        "pokeball": {"position": [0.0, 0.4, -2.5], "radius": 0.5, "button_dir": [0, 0, 1]}}}}
+    sc["xform_in_csg"] = _base([
+        floor,
+        {"union": [t_sph, r_sph]},
+        {"difference": [{"sphere": {"position": [1.3, 0.0, -1.0], "radius": 0.8, "color": _mat([0.3, 0.3, 0.9])}},
+                        t_half]},
+        {"intersection": [s_poke,
+                          {"sphere": {"position": [0.0, 0.9, -2.5], "radius": 0.7, "color": _mat([0.9, 0.6, 0.2])}}]},
+    ], dpi=dpi)
     sc["recursion0"] = copy.deepcopy(sc["reflect_refract"])
     sc["recursion0"]["medium"]["recursion"] = 0
     sc["inside_camera"] = {
