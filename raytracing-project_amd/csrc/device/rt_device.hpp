@@ -764,41 +764,45 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
     R.c1 = (exitE == 0 ? A.c0 : exitE == 1 ? A.c1 : exitE == 2 ? B.c0 : B.c1) | (flipX ? REF_FLIP : 0);
 }
 
-struct CStack {
-    CIvl tos, nos;
-    CIvl spill[kMaxIvlSpill];
-    int sp;   // entries (wave-uniform)
-    __device__ __forceinline__ void push(const CIvl& v) {
-        if (sp >= 2) spill[sp - 2] = nos;
-        if (sp >= 1) nos = tos;
-        tos = v;
-        ++sp;
-    }
-    __device__ __forceinline__ void reduce2(const CIvl& r) {
-        tos = r;
-        if (sp >= 3) nos = spill[sp - 3];
-        --sp;
-    }
-};
-
 // Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
-template <class CT>
+// The top two stack entries are plain locals (VGPRs); only trees that are
+// not left-deep folds touch the spill array (scratch), at uniform indices.
+template <bool DEEP, class CT>
 __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1, const DRay& r, CT& cnt) {
-    CStack st;
-    st.sp = 0;
+    CIvl tos, nos;
+    tos.ok = nos.ok = 0;
+    tos.t0 = tos.t1 = tos.s0 = tos.s1 = nos.t0 = nos.t1 = nos.s0 = nos.s1 = 0.0;
+    tos.c0 = tos.c1 = nos.c0 = nos.c1 = 0;
+    constexpr int NSP = DEEP ? kMaxIvlSpill : 1;
+    double sp_t0[NSP], sp_t1[NSP], sp_s0[NSP], sp_s1[NSP];
+    int sp_ok[NSP], sp_c0[NSP], sp_c1[NSP];
+    int sp = 0;   // stack entries (wave-uniform)
     for (int pc = pc0; pc < pc1; ++pc) {
         const DevOp op = S.ops[pc];
         if (op.op == rtamd::OP_LEAF_IVL) {
             CIvl v;
             leaf_ivl_c(&S.nodes[op.node], pc, r, v, cnt);
-            st.push(v);
+            if (DEEP && sp >= 2) {
+                const int k = sp - 2;
+                sp_ok[k] = nos.ok; sp_t0[k] = nos.t0; sp_t1[k] = nos.t1; sp_s0[k] = nos.s0; sp_s1[k] = nos.s1;
+                sp_c0[k] = nos.c0; sp_c1[k] = nos.c1;
+            }
+            nos = tos;
+            tos = v;
+            ++sp;
         } else {
             CIvl v;
-            csg_c(op.csg_op, st.nos, st.tos, v, cnt);
-            st.reduce2(v);
+            csg_c(op.csg_op, nos, tos, v, cnt);
+            tos = v;
+            if (DEEP && sp >= 3) {
+                const int k = sp - 3;
+                nos.ok = sp_ok[k]; nos.t0 = sp_t0[k]; nos.t1 = sp_t1[k]; nos.s0 = sp_s0[k]; nos.s1 = sp_s1[k];
+                nos.c0 = sp_c0[k]; nos.c1 = sp_c1[k];
+            }
+            --sp;
         }
     }
-    return st.tos;
+    return tos;
 }
 
 // Leaf Primitive::intersect without normal (t and acceptance only).
@@ -871,7 +875,7 @@ __device__ __forceinline__ DRay chain_ray(const DevScene& S, int pc0, int k, con
 
 // Primitive::intersect(object, ray, tmin, tmax): hit t, hit point p and a lazy
 // reference (ts, code) resolved later by resolve_hit().
-template <bool EAGER, class CT>
+template <bool EAGER, bool DEEP, class CT>
 __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, const DRay& world, double tmin,
                                            double tmax, double& t, V3& p, double& ts, int& code, CT& cnt) {
     if (ob.kind <= rtamd::OBJ_POKE) {
@@ -897,7 +901,7 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
             ts = t;
             code = ob.cpc0;
         } else {   // CSG::intersect (csg.cpp:169-185)
-            const CIvl R = run_compact(S, ob.cpc0, ob.cpc1, cur, cnt);
+            const CIvl R = run_compact<DEEP>(S, ob.cpc0, ob.cpc1, cur, cnt);
             t = dmax(R.t0, lo);
             ok = R.ok && (t < R.t1 && t < hi);
             p = v3(cur.o.x + cur.d.x * t, cur.o.y + cur.d.y * t, cur.o.z + cur.d.z * t);
@@ -974,7 +978,7 @@ __device__ __forceinline__ bool bound_touch(const DevObj& ob, const DRay& r, dou
 // Scene::intersect (scene.cpp:10-24): closest hit; every object applies its
 // own accept rule with tmax = closest-so-far, so ties resolve as in the
 // reference (Sphere/HalfSpace accept t == tmax, CSG/transforms do not).
-template <bool EAGER, class CT>
+template <bool EAGER, bool DEEP, class CT>
 __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, double tmax, double& t_best,
                                 DHit& best, CT& cnt) {
     double closest = tmax;
@@ -994,7 +998,7 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
         double t = 0.0, ts = 0.0;
         V3 p;
         int code = 0;
-        if (object_hit<EAGER>(S, ob, r, tmin, closest, t, p, ts, code, cnt)) {
+        if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt)) {
             closest = t;
             win = o;
             wp = p;
@@ -1009,7 +1013,7 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
 }
 
 // Scene::occluded (scene.cpp:33-42): any hit; per-lane early exit.
-template <bool EAGER, class CT>
+template <bool EAGER, bool DEEP, class CT>
 __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, double tmax, CT& cnt) {
     bool hit = false;
     for (int o = 0; o < S.n_objs; ++o) {
@@ -1026,7 +1030,7 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, do
             double t = 0.0, ts = 0.0;
             V3 p;
             int code = 0;
-            hit = object_hit<EAGER>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
+            hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
         }
     }
     return hit;
@@ -1039,7 +1043,7 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 
 // shade_lambert_phong (shading.cpp:31-138), point lights only (the loader
 // never populates directional lights).
-template <bool EAGER, class CT>
+template <bool EAGER, bool DEEP, class CT>
 __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
     if (hit.mat < 0) return v3(1.0, 0.0, 1.0);
     cnt.inc(RT_OPC_SHADE_CALL);
@@ -1064,7 +1068,7 @@ __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32
         const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
         const DRay sr = make_ray(so, wi);
         ++n_occl;
-        if (scene_occluded<EAGER>(S, sr, eps, max_t, cnt)) continue;
+        if (scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt)) continue;
         cnt.inc(RT_OPC_SHADE_LIGHT);
         const double ed = dmax(0.5, dist);
         const double falloff = 1.0 / (ed * ed);
@@ -1099,7 +1103,7 @@ struct Frame {
 };
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
-template <bool EAGER, bool SECONDARY, class CT>
+template <bool EAGER, bool DEEP, bool SECONDARY, class CT>
 __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     if constexpr (!SECONDARY) {
         // No material reflects or refracts (or recursion <= 1): trace_recursive
@@ -1108,8 +1112,8 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         double ht = 0.0;
         DHit h;
         ++n_isect;
-        if (!scene_intersect<EAGER>(S, r, 1e-4, RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
-        return shade<EAGER>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
+        if (!scene_intersect<EAGER, DEEP>(S, r, 1e-4, RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+        return shade<EAGER, DEEP>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
     }
     Frame stk[kMaxDepth];
     int sp = 0;
@@ -1125,11 +1129,11 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
             double ht = 0.0;
             DHit h;
             ++n_isect;
-            if (!scene_intersect<EAGER>(S, r, 1e-4, RT_INF, ht, h, cnt)) {
+            if (!scene_intersect<EAGER, DEEP>(S, r, 1e-4, RT_INF, ht, h, cnt)) {
                 ret = v3(S.bg[0], S.bg[1], S.bg[2]);
             } else {
                 const V3 wo = normalized(vneg(r.d));
-                const V3 direct = shade<EAGER>(S, ht, h, wo, n_occl, cnt);
+                const V3 direct = shade<EAGER, DEEP>(S, ht, h, wo, n_occl, cnt);
                 if (h.mat < 0) {
                     ret = direct;
                 } else {

@@ -67,7 +67,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
     }
 }
 
-template <bool E, bool SEC, bool C>
+template <bool E, bool D, bool SEC, bool C>
 __global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
         const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
         const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)(y - P.jy0) * P.W + x) * 16 + 2 * s);
         const DRay ray = gen_ray_subpixel(S, x, y, j.x, j.y);
-        c = trace<E, SEC>(S, ray, ni, no, cnt);
+        c = trace<E, D, SEC>(S, ray, ni, no, cnt);
     }
     // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
     const int base = lane & ~7;
@@ -127,7 +127,7 @@ struct PaperParams {
     unsigned long long* counters;
 };
 
-template <bool E, bool C>
+template <bool E, bool D, bool C>
 __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
         double ht = 0.0;
         DHit h;
         ++ni;
-        const bool hits = scene_intersect<E>(S, r, 1e-4, RT_INF, ht, h, cnt);
+        const bool hits = scene_intersect<E, D>(S, r, 1e-4, RT_INF, ht, h, cnt);
         const size_t idx = (size_t)ei * P.W + x;
         P.hit[idx] = hits ? 1 : 0;
         P.t[idx] = ht;
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
         if (P.ext_shade[ei]) {
             // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
             V3 base = v3(1.0, 1.0, 1.0);
-            if (hits) base = shade<E>(S, ht, h, normalized(vneg(r.d)), no, cnt);
+            if (hits) base = shade<E, D>(S, ht, h, normalized(vneg(r.d)), no, cnt);
             P.lum[idx] = 0.299 * base.x + 0.587 * base.y + 0.114 * base.z;
         }
     }
@@ -258,29 +258,35 @@ __global__ void k_to_rgb8(const double* __restrict__ fb, size_t n, uint8_t* __re
 }
 
 // Kernel variants: E = scene has eager (transform-inside-CSG) objects,
-// SEC = reflection/refraction frames needed, C = op counting.
-template <bool E, bool SEC>
+// D = some compact CSG needs an interval stack deeper than 2 (not a left-deep
+// fold), SEC = reflection/refraction frames needed, C = op counting.  Eager
+// scenes always use D.  Each variant gets its own register allocation.
+template <bool E, bool D, bool SEC>
 void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std<E, SEC, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std<E, SEC, false>), grid, dim3(256), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_std<E, D, SEC, false>), grid, dim3(256), 0, st, S, P);
 }
-void launch_std(bool e, bool sec, bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
+void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
     if (e) {
-        if (sec) launch_std_c<true, true>(c, grid, st, S, P);
-        else launch_std_c<true, false>(c, grid, st, S, P);
+        if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
+        else launch_std_c<true, true, false>(c, grid, st, S, P);
+    } else if (d) {
+        if (sec) launch_std_c<false, true, true>(c, grid, st, S, P);
+        else launch_std_c<false, true, false>(c, grid, st, S, P);
     } else {
-        if (sec) launch_std_c<false, true>(c, grid, st, S, P);
-        else launch_std_c<false, false>(c, grid, st, S, P);
+        if (sec) launch_std_c<false, false, true>(c, grid, st, S, P);
+        else launch_std_c<false, false, false>(c, grid, st, S, P);
     }
 }
-void launch_paper(bool e, bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
-    if (e) {
-        if (c) hipLaunchKernelGGL((k_paper_primary<true, true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary<true, false>), grid, dim3(256), 0, st, S, P);
-    } else {
-        if (c) hipLaunchKernelGGL((k_paper_primary<false, true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary<false, false>), grid, dim3(256), 0, st, S, P);
-    }
+template <bool E, bool D>
+void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
+    if (c) hipLaunchKernelGGL((k_paper_primary<E, D, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary<E, D, false>), grid, dim3(256), 0, st, S, P);
+}
+void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
+    if (e) launch_paper_c<true, true>(c, grid, st, S, P);
+    else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
+    else launch_paper_c<false, false>(c, grid, st, S, P);
 }
 
 // ------------------------------------------------------------ host side
@@ -367,7 +373,8 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     bool secondary = false;
     for (int i = 0; i < d.n_materials; ++i)
         if (d.materials[i].kr > 0.0 || d.materials[i].kt > 0.0) secondary = true;
-    if (d.recursion_limit < 2) secondary = false;   // depth < limit-1 never holds (tracer.cpp:38,51)
+    if (d.recursion_limit < 2) secondary = false;
+    const bool deep = cs.max_ivl_depth > 2;   // depth < limit-1 never holds (tracer.cpp:38,51)
     if (secondary && mode == RT_MODE_STANDARD && d.recursion_limit - 1 > kMaxDepth) {
         rtamd::set_last_error("medium.recursion exceeds the device frame stack (17)");
         return RT_ERR_UNSUPPORTED;
@@ -455,7 +462,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
             P.fb = fb_dev;
             P.counters = ctr;
             dim3 grid((W + 7) / 8, (n_rows + 3) / 4);
-            launch_std(cs.has_eager, secondary, count_ops, grid, st, S, P);
+            launch_std(cs.has_eager, deep, secondary, count_ops, grid, st, S, P);
             HIP_TRY(hipGetLastError());
             HIP_TRY(hipEventRecord(ws.ev[2], st));
         } else {
@@ -517,7 +524,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
             HIP_TRY(hipEventRecord(ws.ev[0], st));
             HIP_TRY(hipEventRecord(ws.ev[1], st));
             dim3 g1((W + 15) / 16, (n_ext + 15) / 16);
-            launch_paper(cs.has_eager, count_ops, g1, st, S, P);
+            launch_paper(cs.has_eager, deep, count_ops, g1, st, S, P);
             HIP_TRY(hipGetLastError());
             dim3 g2((W + 63) / 64, (n_rows + 3) / 4);
             hipLaunchKernelGGL(k_paper_finish, g2, dim3(256), 0, st, P);
