@@ -28,7 +28,6 @@ sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: 256 CU x 64 lanes x 2 x 2.4 GHz
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table
-STRIP = 8                      # rows per interleaved strip (multi-GPU)
 
 
 def model_flops(ops: dict, primary: int, paper: bool) -> tuple[float, dict]:
@@ -47,14 +46,6 @@ def model_flops(ops: dict, primary: int, paper: bool) -> tuple[float, dict]:
     f += 38 * (ops["shade_light"] - ops["shade_spec"]) + 80 * ops["shade_spec"]
     f += 70 * ops["secondary"]
     return float(f), {"pow": ops["shade_spec"], "acos": ops["poke_region"]}
-
-
-def strip_rows(H: int, rank: int, world: int) -> list[int]:
-    rows = []
-    for s in range((H + STRIP - 1) // STRIP):
-        if s % world == rank:
-            rows.extend(range(s * STRIP, min(H, (s + 1) * STRIP)))
-    return rows
 
 
 def main() -> int:
@@ -81,8 +72,10 @@ def main() -> int:
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    import frame_dist
     import rtamd
     import scenes
+    from frame_dist import STRIP, strip_rows
 
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
@@ -94,7 +87,7 @@ def main() -> int:
     rows = strip_rows(H, rank, world)
     n_rows = len(rows)
     rows_c = (C.c_int32 * max(1, n_rows))(*rows)
-    max_rows = len(strip_rows(H, 0, world))
+    max_rows = frame_dist.max_rows(H, world)
     fb_rows = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)
     full = torch.zeros((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
     gathered = None
@@ -102,11 +95,7 @@ def main() -> int:
     if world > 1:
         gathered = torch.zeros((world * max_rows, W, 3), dtype=torch.float64, device=dev) if True else None
         if rank == 0:
-            cat = []
-            for r in range(world):
-                rr = strip_rows(H, r, world)
-                cat.extend(rr + [-1] * (max_rows - len(rr)))
-            all_rows_dev = torch.tensor(cat, dtype=torch.int32, device=dev)
+            all_rows_dev = torch.tensor(frame_dist.gather_row_index(H, world), dtype=torch.int32, device=dev)
 
     stream = torch.cuda.current_stream(dev)
     st = rtamd.Stats()

@@ -1,0 +1,28 @@
+/*
+ * rt_test.h — test hooks exported by librtamd.so (not part of the drop-in
+ * boundary; used by tests/ to check the jitter-stream machinery in isolation).
+ */
+#ifndef RT_TEST_H
+#define RT_TEST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* CPU check of the GF(2) jump polynomials (csrc/host/mt_poly.cpp): for
+ * levels j < levels, applying x^(624*K*2^j) mod phi to the first window must
+ * equal advancing it K*2^j twist blocks sequentially.  Returns the number of
+ * mismatching levels (0 = all good), -1 on error. */
+int rt_test_mt_jump_cpu(int K_blocks, int levels);
+
+/* GPU: generate the jitter stream for output indices [q0, q1) (even) with the
+ * device jump/fill kernels and copy uniform draws [first, first+count) (draw
+ * index = output index / 2) to out_host.  Returns an rt_status. */
+int rt_test_jitter_device(int64_t q0, int64_t q1, int64_t first, int64_t count, double* out_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "mt_jump.hpp"
 
 namespace {
@@ -64,38 +66,32 @@ __device__ __forceinline__ void twist_blocks(uint32_t* buf, int nblocks, int lim
     }
 }
 
-// One workgroup per segment: window(c) = jumps for every set bit of c applied
-// to the base window (outputs 0..623).
-__global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint32_t* __restrict__ base_win,
-                                                          const uint32_t* __restrict__ polys, int levels,
-                                                          int64_t c0, uint32_t* __restrict__ ckpt) {
+// Tree doubling, level j: ckpt[c] = jump(ckpt[c - 2^j]) by x^(624*K*2^j) for
+// c in [lo, lo + gridDim.x).  The jump is the correlation
+// out[j] = XOR_{i in taps} w[i + j] over the raw words regenerated from the
+// source window; taps = exponents with a 1 coefficient (host-built list).
+__global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump_level(const uint32_t* __restrict__ taps, int ntaps,
+                                                                int64_t lo, int64_t stride,
+                                                                uint32_t* __restrict__ ckpt) {
     __shared__ uint32_t buf[JUMP_BUF + 8];
-    const int64_t c = c0 + blockIdx.x;
+    const int64_t c = lo + blockIdx.x;
     const int tid = threadIdx.x;
-    uint32_t win = (tid < N) ? base_win[tid] : 0u;
-    for (int k = 0; k < levels; ++k) {
-        if (!((c >> k) & 1)) continue;   // wave-uniform
-        if (tid < N) buf[tid] = win;
-        __syncthreads();
-        twist_blocks(buf, (JUMP_BUF - N + N - 1) / N, JUMP_BUF);
-        // correlation: out[j] = XOR_{i: p_i = 1} w[i + j]
-        const uint32_t* P = polys + (size_t)k * N;
-        uint32_t acc = 0;
-        if (tid < N) {
-            for (int wi = 0; wi < N; ++wi) {
-                uint32_t bits = P[wi];   // uniform -> scalar load
-                const uint32_t* src = buf + wi * 32 + tid;
-                while (bits) {
-                    const int b = __builtin_ctz(bits);
-                    acc ^= src[b];
-                    bits &= bits - 1u;
-                }
-            }
+    for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)(c - stride) * N + j];
+    __syncthreads();
+    twist_blocks(buf, (JUMP_BUF - 1) / N, JUMP_BUF);
+    if (tid < N) {
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        const uint32_t* src = buf + tid;
+        int i = 0;
+        for (; i + 4 <= ntaps; i += 4) {   // taps[i] are wave-uniform (scalar loads)
+            a0 ^= src[taps[i]];
+            a1 ^= src[taps[i + 1]];
+            a2 ^= src[taps[i + 2]];
+            a3 ^= src[taps[i + 3]];
         }
-        __syncthreads();
-        win = acc;
+        for (; i < ntaps; ++i) a0 ^= src[taps[i]];
+        ckpt[(size_t)c * N + tid] = a0 ^ a1 ^ a2 ^ a3;
     }
-    if (tid < N) ckpt[(size_t)blockIdx.x * N + tid] = win;
 }
 
 // One workgroup per segment: regenerate K blocks from the checkpoint and
@@ -104,7 +100,7 @@ __global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __rest
                                                           int64_t q0, int64_t q1, double* __restrict__ jit) {
     __shared__ uint32_t buf[2 * N + 8];
     const int tid = threadIdx.x;
-    for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)blockIdx.x * N + j];
+    for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)(c0 + blockIdx.x) * N + j];
     __syncthreads();
     const int64_t seg_q = (c0 + blockIdx.x) * (int64_t)K * N;
     for (int b = 0; b < K; ++b) {
@@ -129,24 +125,30 @@ __global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __rest
 
 namespace rtamd {
 
-hipError_t mt_launch_jitter(const uint32_t* d_base_win, const uint32_t* d_polys, int levels, int K,
-                            int64_t q0, int64_t q1, uint32_t* d_ckpt, double* d_jit, hipStream_t stream) {
+hipError_t mt_launch_jitter(const uint32_t* d_base_win, const uint32_t* d_taps, const int32_t* tap_off, int levels,
+                            int K, int64_t q0, int64_t q1, uint32_t* d_ckpt, double* d_jit, hipStream_t stream) {
     if (q1 <= q0) return hipSuccess;
     const int64_t seg = (int64_t)K * N;
     const int64_t c0 = q0 / seg, c1 = (q1 - 1) / seg;
-    const int64_t nseg = c1 - c0 + 1;
-    hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)nseg), dim3(JUMP_THREADS), 0, stream, d_base_win, d_polys, levels,
-                       c0, d_ckpt);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipMemcpyAsync(d_ckpt, d_base_win, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mt_fill, dim3((unsigned)nseg), dim3(FILL_THREADS), 0, stream, d_ckpt, K, c0, q0, q1, d_jit);
+    for (int j = 0; j < levels; ++j) {
+        const int64_t lo = (int64_t)1 << j;
+        if (lo > c1) break;
+        const int64_t hi = std::min<int64_t>((int64_t)2 << j, c1 + 1);
+        hipLaunchKernelGGL(k_mt_jump_level, dim3((unsigned)(hi - lo)), dim3(JUMP_THREADS), 0, stream,
+                           d_taps + tap_off[j], tap_off[j + 1] - tap_off[j], lo, lo, d_ckpt);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_mt_fill, dim3((unsigned)(c1 - c0 + 1)), dim3(FILL_THREADS), 0, stream, d_ckpt, K, c0, q0,
+                       q1, d_jit);
     return hipGetLastError();
 }
 
-int64_t mt_num_segments(int K, int64_t q0, int64_t q1) {
-    if (q1 <= q0) return 0;
-    const int64_t seg = (int64_t)K * N;
-    return (q1 - 1) / seg - q0 / seg + 1;
+int64_t mt_num_checkpoints(int K, int64_t q1) {
+    if (q1 <= 0) return 1;
+    return (q1 - 1) / ((int64_t)K * N) + 1;
 }
 
 int mt_levels_needed(int K, int64_t q1) {

@@ -1,0 +1,108 @@
+"""C-ABI libraries: exports, host helpers (PNG writer, toByte), CLI error
+paths and the jump-ahead polynomials.  No GPU compute here."""
+import ctypes as C
+import json
+import os
+import re
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+INCLUDE = os.path.join(REPO, "include")
+LIB = os.path.join(REPO, "raytracing-project_amd", "lib")
+RAY = os.path.join(REPO, "raytracing-project_amd", "bin", "ray")
+
+
+def _declared_functions(header):
+    text = open(os.path.join(INCLUDE, header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(rt_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_libraries_export_every_declared_symbol():
+    host = C.CDLL(os.path.join(LIB, "librt_host.so"), mode=C.RTLD_GLOBAL)
+    amd = C.CDLL(os.path.join(LIB, "librtamd.so"), mode=C.RTLD_GLOBAL)
+    declared = _declared_functions("rt.h") + _declared_functions("rt_test.h")
+    assert len(declared) >= 18 and "rt_render" in declared and "rt_last_error" in declared
+    for name in declared:
+        assert hasattr(host, name) or hasattr(amd, name), name
+    assert amd.rt_abi_version() == 1
+
+
+def _decode_png(path):
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, W = 8, b"", None
+    while pos < len(data):
+        n, typ = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        crc = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])[0]
+        assert zlib.crc32(typ + body) & 0xFFFFFFFF == crc
+        if typ == b"IHDR":
+            W, H, depth, ctype = struct.unpack(">IIBB", body[:10])
+            assert depth == 8 and ctype == 2
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    rows = np.frombuffer(raw, dtype=np.uint8).reshape(H, 1 + 3 * W)
+    assert (rows[:, 0] == 0).all()
+    return rows[:, 1:].reshape(H, W, 3)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_png_roundtrip(rt, tmp_path, threads):
+    rng = np.random.default_rng(threads)
+    img = rng.integers(0, 256, size=(37, 53, 3), dtype=np.uint8)
+    p = str(tmp_path / "x.png")
+    rt.write_png(p, img, threads=threads)
+    assert np.array_equal(_decode_png(p), img)
+
+
+def test_to_rgb8_matches_toByte(rt):
+    # toByte(v) = (int)std::round(clamp01(v) * 255): round half away from zero (core.h:313-316)
+    v = np.array([-1.0, 0.0, 0.5 / 255, 1.5 / 255, 0.5, 127.5 / 255, 1.0, 1.2, np.nan, 0.999999, 2.5 / 255, 1e-300])
+    v = np.pad(v, (0, (-len(v)) % 3)).reshape(-1, 1, 3)
+    got = rt.to_rgb8(v).reshape(-1)
+    flat = v.reshape(-1)
+    clamped = np.where(flat < 1.0, flat, 1.0)   # std::min(1.0, v) maps NaN to 1
+    clamped = np.where(0.0 < clamped, clamped, 0.0)
+    want = np.floor(clamped * 255.0 + 0.5).astype(np.uint8)
+    assert np.array_equal(got, want)
+
+
+def test_mt19937_jump_polynomials_cpu():
+    amd = C.CDLL(os.path.join(LIB, "librtamd.so"), mode=C.RTLD_GLOBAL)
+    assert amd.rt_test_mt_jump_cpu(1024, 4) == 0
+    assert amd.rt_test_mt_jump_cpu(3, 5) == 0   # non power-of-two segment length
+
+
+def test_cli_usage_and_load_errors(tmp_path):
+    r = subprocess.run([RAY], capture_output=True, text=True)
+    assert r.returncode == 1 and "Usage:" in r.stderr and "--paper" in r.stderr
+    r = subprocess.run([RAY, str(tmp_path / "missing.json"), str(tmp_path / "o.png")], capture_output=True, text=True)
+    assert r.returncode == 3 and r.stderr.startswith("[error] Cannot open JSON file: ")
+    bad = tmp_path / "bad.json"
+    bad.write_text("{ invalid json }")
+    r = subprocess.run([RAY, str(bad), str(tmp_path / "o.png")], capture_output=True, text=True)
+    assert r.returncode == 3 and r.stderr.startswith("[error] JSON parse error: ")
+    bad.write_text(json.dumps({"objects": [{"sphere": {"position": [0, 0, 0], "radius": 1, "color": [1, 0, 0]}}]}))
+    r = subprocess.run([RAY, str(bad), str(tmp_path / "o.png")], capture_output=True, text=True)
+    assert r.returncode == 3 and "JSON processing error: color must be an object" in r.stderr
+
+
+def test_render_without_device_fails_loudly(rt):
+    """On a host without a HIP device the product path errors out (no CPU fallback)."""
+    amd = rt.amd_lib()
+    if amd.rt_device_count() > 0:
+        pytest.skip("a GPU is present")
+    sc = rt.load_scene_from_json_text(json.dumps({"objects": []}))
+    with pytest.raises(rt.RTError) as e:
+        rt.Tracer(sc, 4, 4, 0).render()
+    assert e.value.code == -7
