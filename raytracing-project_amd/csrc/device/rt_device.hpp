@@ -653,6 +653,35 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
     R.c0 = R.c1 = 0;
     if (!A.ok && !B.ok) return;
     cnt.inc(RT_OPC_CSG_COMBINE);
+    if (!(A.ok && B.ok)) {
+        // Exactly one operand has an interval X.  The sweep then sees only X's
+        // events: an intersection is never inside; a difference without A is
+        // never inside; otherwise the result is X itself, or, when the origin
+        // lies inside X, [0, X.t1] with the inside-at-origin entry hit
+        // (csg.cpp:113-122).  An infinite exit gives no hit (:158); an
+        // infinite entry outside the origin gives no entry (:134-146).
+        const bool useA = A.ok;
+        if (op == RT_CSG_INTERSECTION || (op == RT_CSG_DIFFERENCE && !useA)) return;
+        const CIvl& X = useA ? A : B;
+        const bool inX = (X.t0 < 1e-6) && (X.t1 > 1e-6);
+        R.t1 = X.t1;
+        R.s1 = X.s1;
+        R.c1 = X.c1;
+        if (inX) {
+            R.ok = __builtin_isfinite(X.t1);
+            R.t0 = 0.0;
+            R.s0 = X.s0;
+            R.c0 = (X.c0 & ~REF_FLIP) | REF_ORIGIN;
+        } else {
+            // two events sorted by the same epsilon comparator: an exit that
+            // sorts first (t1 < t0 - 1e-6, possible for CSG results) never closes
+            R.ok = __builtin_isfinite(X.t0) && __builtin_isfinite(X.t1) && !ev_less(X.t1, 1, X.t0, 0);
+            R.t0 = X.t0;
+            R.s0 = X.s0;
+            R.c0 = X.c0;
+        }
+        return;
+    }
     // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
     double et[4];
     int ec[4];
