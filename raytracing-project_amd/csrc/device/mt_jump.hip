@@ -69,55 +69,75 @@ __device__ __forceinline__ void twist_blocks(uint32_t* buf, int nblocks, int lim
 // Tree doubling, level j: ckpt[c] = jump(ckpt[c - 2^j]) by x^(624*K*2^j) for
 // c in [lo, lo + gridDim.x).  The jump is the correlation
 // out[j] = XOR_{i in taps} w[i + j] over the raw words regenerated from the
-// source window; taps = exponents with a 1 coefficient (host-built list).
+// source window; taps = exponents with a 1 coefficient (host-built list,
+// staged in LDS as 16-bit offsets and read 8 at a time by broadcast).
+constexpr int MAX_TAPS = DEG + 8;
 __global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump_level(const uint32_t* __restrict__ taps, int ntaps,
                                                                 int64_t lo, int64_t stride,
                                                                 uint32_t* __restrict__ ckpt) {
     __shared__ uint32_t buf[JUMP_BUF + 8];
+    __shared__ __attribute__((aligned(16))) uint16_t tp[MAX_TAPS];
     const int64_t c = lo + blockIdx.x;
     const int tid = threadIdx.x;
     for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)(c - stride) * N + j];
+    const int n8 = ntaps & ~7;
+    for (int i = tid; i < ntaps; i += blockDim.x) tp[i] = (uint16_t)taps[i];
     __syncthreads();
     twist_blocks(buf, (JUMP_BUF - 1) / N, JUMP_BUF);
     if (tid < N) {
         uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
         const uint32_t* src = buf + tid;
-        int i = 0;
-        for (; i + 4 <= ntaps; i += 4) {   // taps[i] are wave-uniform (scalar loads)
-            a0 ^= src[taps[i]];
-            a1 ^= src[taps[i + 1]];
-            a2 ^= src[taps[i + 2]];
-            a3 ^= src[taps[i + 3]];
+        for (int i = 0; i < n8; i += 8) {
+            const uint4 q = *reinterpret_cast<const uint4*>(tp + i);   // uniform address: broadcast
+            a0 ^= src[q.x & 0xffffu];
+            a1 ^= src[q.x >> 16];
+            a2 ^= src[q.y & 0xffffu];
+            a3 ^= src[q.y >> 16];
+            a0 ^= src[q.z & 0xffffu];
+            a1 ^= src[q.z >> 16];
+            a2 ^= src[q.w & 0xffffu];
+            a3 ^= src[q.w >> 16];
         }
-        for (; i < ntaps; ++i) a0 ^= src[taps[i]];
+        for (int i = n8; i < ntaps; ++i) a0 ^= src[tp[i]];
         ckpt[(size_t)c * N + tid] = a0 ^ a1 ^ a2 ^ a3;
     }
 }
 
 // One workgroup per segment: regenerate K blocks from the checkpoint and
-// write jitter for outputs in [q0, q1).
+// write jitter for outputs in [q0, q1).  buf is a 2-block ring: the block at
+// offset `base` is converted to jitter while the first twist phase of the
+// next block (written at base + 624, mod 1248) runs; no copies.
 __global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __restrict__ ckpt, int K, int64_t c0,
                                                           int64_t q0, int64_t q1, double* __restrict__ jit) {
-    __shared__ uint32_t buf[2 * N + 8];
+    __shared__ uint32_t buf[2 * N];
     const int tid = threadIdx.x;
     for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)(c0 + blockIdx.x) * N + j];
     __syncthreads();
     const int64_t seg_q = (c0 + blockIdx.x) * (int64_t)K * N;
+    int base = 0;
     for (int b = 0; b < K; ++b) {
-        const int64_t bq = seg_q + (int64_t)b * N;   // output index of buf[0]
+        const int64_t bq = seg_q + (int64_t)b * N;   // output index of the block at `base`
         if (bq >= q1) break;                          // uniform
+        const bool more = b + 1 < K && bq + N < q1;   // uniform
+        const int nb = base ^ N;                      // ring slot of the next block (0 <-> 624)
+        auto R = [&](int k) { return buf[(base + k) % (2 * N)]; };
+        // phase 1 of the next block + conversion of this block
+        if (more)
+            for (int j = tid; j < 227; j += blockDim.x) buf[nb + j] = twist_word(R(j), R(j + 1), R(j + 397));
         if (bq + N > q0) {
             for (int i = tid; i < N / 2; i += blockDim.x) {
                 const int64_t q = bq + 2 * i;
-                if (q >= q0 && q < q1)
-                    jit[(q - q0) >> 1] = jitter_from(temper(buf[2 * i]), temper(buf[2 * i + 1]));
+                if (q >= q0 && q < q1) jit[(q - q0) >> 1] = jitter_from(temper(R(2 * i)), temper(R(2 * i + 1)));
             }
         }
-        if (b + 1 < K && bq + N < q1) {
-            twist_blocks(buf, 1, 2 * N);
-            for (int j = tid; j < N; j += blockDim.x) buf[j] = buf[N + j];
+        __syncthreads();
+        if (more) {
+            for (int j = 227 + tid; j < 454; j += blockDim.x) buf[nb + j] = twist_word(R(j), R(j + 1), R(j + 397));
+            __syncthreads();
+            for (int j = 454 + tid; j < N; j += blockDim.x) buf[nb + j] = twist_word(R(j), R(j + 1), R(j + 397));
             __syncthreads();
         }
+        base = nb;
     }
 }
 

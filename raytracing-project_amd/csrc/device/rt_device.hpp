@@ -1018,6 +1018,13 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
     for (int o = 0; o < S.n_objs; ++o) {
         const DevObj ob = S.objs[o];
         if (ob.kind == rtamd::OBJ_NEVER) continue;
+        if (ob.kind == rtamd::OBJ_GROUP) {
+            if (S.cull && !__any(bound_touch(ob, r, tmin, closest))) {
+                cnt.inc(RT_OPC_CULLED);
+                o += ob.m;
+            }
+            continue;
+        }
         if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound && S.cull) {
             if (!__any(bound_touch(ob, r, tmin, closest))) {
                 cnt.inc(RT_OPC_CULLED);
@@ -1049,6 +1056,13 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, do
         if (__all(hit)) break;
         const DevObj ob = S.objs[o];
         if (ob.kind == rtamd::OBJ_NEVER) continue;
+        if (ob.kind == rtamd::OBJ_GROUP) {
+            if (S.cull && !__any(!hit && bound_touch(ob, r, tmin, tmax))) {
+                cnt.inc(RT_OPC_CULLED);
+                o += ob.m;
+            }
+            continue;
+        }
         if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound && S.cull) {
             if (!__any(!hit && bound_touch(ob, r, tmin, tmax))) {
                 cnt.inc(RT_OPC_CULLED);

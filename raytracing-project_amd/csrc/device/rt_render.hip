@@ -30,6 +30,7 @@ using namespace rtd;
 namespace {
 
 constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
+constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics
 constexpr int kJitterK = 1024;          // twist blocks per jitter segment
 
 struct StdParams {
@@ -42,28 +43,35 @@ struct StdParams {
     unsigned long long* counters;
 };
 
+// Ray / op counters: wave reduction by shuffles, block reduction through LDS,
+// then one atomic per block and counter into one of kCounterSlots slots
+// (blockIdx-hashed).  A single hot address would serialize ~2M atomics at the
+// L2 (~6 ns each, MI355X_MICROARCH.md fan-in row) - 12 ms per 4K frame.
 template <bool C>
 __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
-    // wave reduction, one atomic per wave and counter
-    unsigned long long a = ni, b = no;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_xor(a, off);
-        b += __shfl_xor(b, off);
-    }
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) {
-        if (a) atomicAdd(&ctr[0], a);
-        if (b) atomicAdd(&ctr[1], b);
-    }
+    constexpr int NW = C ? 18 : 2;
+    __shared__ unsigned long long red[4][NW];
+    unsigned long long v[NW];
+    v[0] = ni;
+    v[1] = no;
     if constexpr (C) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            unsigned long long v = cnt.c[k];
+        for (int k = 0; k < 16; ++k) v[2 + k] = cnt.c[k];
+    }
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if (lane == 0 && v) atomicAdd(&ctr[2 + k], v);
-        }
+    for (int k = 0; k < NW; ++k)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NW; ++k) red[wave][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < NW) {
+        const unsigned long long sum = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                       red[3][threadIdx.x];
+        const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x) % kCounterSlots;
+        if (sum) atomicAdd(&ctr[(size_t)slot * kCounterWords + threadIdx.x], sum);
     }
 }
 
@@ -396,8 +404,9 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     HIP_TRY(upload(ws.lights, lights, st));
     HIP_TRY(upload(ws.objs, cs.objs, st));
     HIP_TRY(upload(ws.ops, cs.ops, st));
-    HIP_TRY(ws.counters.ensure(kCounterWords * sizeof(unsigned long long)));
-    HIP_TRY(hipMemsetAsync(ws.counters.p, 0, kCounterWords * sizeof(unsigned long long), st));
+    const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
+    HIP_TRY(ws.counters.ensure(ctr_bytes));
+    HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
 
     DevScene S;
     S.nodes = ws.nodes.as<rt_node>();
@@ -546,9 +555,12 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
         HIP_TRY(hipEventRecord(ws.ev[1], st));
         HIP_TRY(hipEventRecord(ws.ev[2], st));
     }
-    unsigned long long hc[kCounterWords];
-    HIP_TRY(hipMemcpyAsync(hc, ctr, sizeof(hc), hipMemcpyDeviceToHost, st));
+    std::vector<unsigned long long> slots((size_t)kCounterSlots * kCounterWords);
+    HIP_TRY(hipMemcpyAsync(slots.data(), ctr, ctr_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    unsigned long long hc[kCounterWords] = {};
+    for (int sl = 0; sl < kCounterSlots; ++sl)
+        for (int k = 0; k < kCounterWords; ++k) hc[k] += slots[(size_t)sl * kCounterWords + k];
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
         stats->rays_intersect = mode == RT_MODE_PAPER ? logical_isect : hc[0];

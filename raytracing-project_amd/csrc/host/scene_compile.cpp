@@ -265,7 +265,46 @@ public:
         }
         cs.max_ray_depth = max_r_;
         cs.max_ivl_depth = max_i_;
+        cs.objs = insert_groups(cs.objs);
         return cs;
+    }
+
+    // Wave-uniform cull groups over runs of consecutive bounded objects.  A run
+    // grows while its bounding ball stays within 2x the largest member radius
+    // (so it is worth testing) and has at most 8 members; only runs of >= 2
+    // members get a header.  Skipping a run is exact: no object in it can
+    // report a hit for a lane whose segment misses the bound.
+    static std::vector<DevObj> insert_groups(const std::vector<DevObj>& in) {
+        std::vector<DevObj> out;
+        size_t i = 0;
+        while (i < in.size()) {
+            if (!in[i].has_bound) { out.push_back(in[i]); ++i; continue; }
+            Bound g = ball(in[i].bc[0], in[i].bc[1], in[i].bc[2], in[i].br);
+            double rmax = in[i].br;
+            size_t j = i + 1;
+            while (j < in.size() && in[j].has_bound && j - i < 8) {
+                Bound b = ball(in[j].bc[0], in[j].bc[1], in[j].bc[2], in[j].br);
+                Bound m = merge_union(g, b);
+                const double r2 = std::max(rmax, in[j].br);
+                if (m.r > 2.0 * r2) break;
+                g = m;
+                rmax = r2;
+                ++j;
+            }
+            if (j - i >= 2) {
+                DevObj h{};
+                h.kind = OBJ_GROUP;
+                h.m = (int)(j - i);
+                h.has_bound = 1;
+                const double mag = std::fabs(g.c[0]) + std::fabs(g.c[1]) + std::fabs(g.c[2]) + g.r;
+                for (int k = 0; k < 3; ++k) h.bc[k] = g.c[k];
+                h.br = g.r * (1.0 + 1e-7) + 1e-7 * (1.0 + mag);
+                out.push_back(h);
+            }
+            for (size_t k = i; k < j; ++k) out.push_back(in[k]);
+            i = j;
+        }
+        return out;
     }
 
 private:

@@ -29,7 +29,8 @@ enum DevObjKind : int32_t {
     OBJ_POKE = 2,
     OBJ_CHAIN = 3,
     OBJ_EAGER = 4,
-    OBJ_NEVER = 5
+    OBJ_NEVER = 5,
+    OBJ_GROUP = 6       // cull header: the next m objects lie inside bound (skipped when no lane touches it)
 };
 
 enum DevOpCode : int32_t {
@@ -47,7 +48,7 @@ struct DevObj {
     int32_t kind;
     int32_t node;       // leaf node (bare leaves; CHAIN with a leaf core)
     int32_t pc0;        // CHAIN: first XPUSH op; EAGER: program start
-    int32_t m;          // CHAIN: number of transforms in the chain
+    int32_t m;          // CHAIN: number of transforms in the chain; GROUP: member count
     int32_t core;       // CHAIN: 0 = leaf core, 1 = CSG core
     int32_t cpc0, cpc1; // CHAIN: leaf core -> cpc0 = its LEAF_ISECT op; CSG core -> [cpc0,cpc1) compact program
     int32_t pc1;        // EAGER: program end
