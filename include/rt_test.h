@@ -22,6 +22,13 @@ int rt_test_mt_jump_cpu(int K_blocks, int levels);
  * index = output index / 2) to out_host.  Returns an rt_status. */
 int rt_test_jitter_device(int64_t q0, int64_t q1, int64_t first, int64_t count, double* out_host);
 
+/* Host-only: compile a scene to its device object table and report
+ * out[8] = {objects incl. cull headers, object cull groups, their members,
+ * program ops, CSG operand groups (OP_IVL_GROUP), their members, has eager
+ * programs, max CSG operand depth}.  No device is touched. */
+struct rt_scene;
+int rt_test_compile_info(const struct rt_scene* s, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -106,6 +106,7 @@ struct DevScene {
     const rt_light* lights;
     const DevObj* objs;
     const DevOp* ops;
+    const double* gb;   // OP_IVL_GROUP bounds (cx, cy, cz, r)
     int n_lights, n_objs;
     int cam_nx, cam_ny;
     int rec_limit, cull;
@@ -793,6 +794,18 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
     R.c1 = (exitE == 0 ? A.c0 : exitE == 1 ? A.c1 : exitE == 2 ? B.c0 : B.c1) | (flipX ? REF_FLIP : 0);
 }
 
+// Can the full line of r meet the ball g = (cx, cy, cz, r)?  Conservative:
+// a lane answering "no" gets an empty Primitive::interval from every sphere
+// inside g (the radius is inflated and the disc test has an absolute margin
+// well above its rounding error).
+__device__ __forceinline__ bool line_touch(const double* g, const DRay& r) {
+    const V3 oc = v3(r.o.x - g[0], r.o.y - g[1], r.o.z - g[2]);
+    const double b = dot3(oc, r.d);
+    const double c2 = dot3(oc, oc);
+    const double disc = b * b - (c2 - g[3] * g[3]);
+    return !(disc < -(1e-9 * c2 + 1e-12));
+}
+
 // Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
 // The top two stack entries are plain locals (VGPRs); only trees that are
 // not left-deep folds touch the spill array (scratch), at uniform indices.
@@ -819,6 +832,17 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
             nos = tos;
             tos = v;
             ++sp;
+        } else if (op.op == rtamd::OP_IVL_GROUP) {
+            if (S.cull && !__any(line_touch(S.gb + 4 * op.node, r))) {
+                cnt.inc(RT_OPC_CULLED);
+                CIvl e, v;
+                e.ok = 0;
+                e.t0 = e.t1 = e.s0 = e.s1 = 0.0;
+                e.c0 = e.c1 = 0;
+                csg_c(op.csg_op, tos, e, v, cnt);
+                tos = v;
+                pc += op.top;
+            }
         } else {
             CIvl v;
             csg_c(op.csg_op, nos, tos, v, cnt);

@@ -328,7 +328,7 @@ struct DBuf {
 // Per-device workspace (one render at a time per device; guarded by a mutex).
 struct Workspace {
     std::mutex mu;
-    DBuf nodes, mats, lights, objs, ops;
+    DBuf nodes, mats, lights, objs, ops, gb;
     DBuf rows, jit, ckpt, polys, basewin, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
     int polys_levels = 0;
@@ -404,6 +404,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     HIP_TRY(upload(ws.lights, lights, st));
     HIP_TRY(upload(ws.objs, cs.objs, st));
     HIP_TRY(upload(ws.ops, cs.ops, st));
+    HIP_TRY(upload(ws.gb, cs.gbounds, st));
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
@@ -414,6 +415,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     S.lights = ws.lights.as<rt_light>();
     S.objs = ws.objs.as<DevObj>();
     S.ops = ws.ops.as<DevOp>();
+    S.gb = ws.gb.as<double>();
     S.n_lights = d.n_lights;
     S.n_objs = (int)cs.objs.size();
     S.cam_nx = rt_camera_width(&d.camera);
@@ -699,4 +701,28 @@ extern "C" int rt_test_jitter_device(int64_t q0, int64_t q1, int64_t first, int6
     (void)hipFree(dc.p);
     (void)hipFree(dj.p);
     return RT_OK;
+}
+
+extern "C" int rt_test_compile_info(const rt_scene* s, int32_t* out) {
+    if (!s || !out) return RT_ERR_INVALID_ARG;
+    try {
+        const rtamd::CompiledScene cs = rtamd::compile_scene(*rt_scene_get_desc(s));
+        int groups = 0, members = 0, ivl_groups = 0, ivl_members = 0;
+        for (const auto& o : cs.objs)
+            if (o.kind == rtamd::OBJ_GROUP) { ++groups; members += o.m; }
+        for (const auto& op : cs.ops)
+            if (op.op == rtamd::OP_IVL_GROUP) { ++ivl_groups; ivl_members += op.top / 2; }
+        out[0] = (int32_t)cs.objs.size();
+        out[1] = groups;
+        out[2] = members;
+        out[3] = (int32_t)cs.ops.size();
+        out[4] = ivl_groups;
+        out[5] = ivl_members;
+        out[6] = cs.has_eager ? 1 : 0;
+        out[7] = cs.max_ivl_depth;
+        return RT_OK;
+    } catch (const std::exception& e) {
+        rtamd::set_last_error(std::string("scene compile: ") + e.what());
+        return RT_ERR_INVALID_ARG;
+    }
 }

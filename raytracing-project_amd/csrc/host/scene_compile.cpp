@@ -188,23 +188,100 @@ public:
         }
     }
 
+    // Compact interval program of a CSG subtree.  A left-deep fold of one
+    // operator (the loader's n-ary arrays, json_loader.cpp:375-401) is
+    // emitted as a0, b1, CSG, b2, CSG, ...; runs of consecutive sphere /
+    // pokeball operands b_i..b_j may get an OP_IVL_GROUP header.  Skipping a
+    // run is exact: a leaf whose line misses its sphere has an empty
+    // interval, and combining the running interval with an empty one is
+    // idempotent (csg_c: A op empty = f(A) with f(f(A)) = f(A)), so m skipped
+    // steps equal one combine with an empty interval.
+    //
+    // The runs are chosen by dynamic programming over the fold order with the
+    // cost model "a header costs one leaf test and is passed by a fraction
+    // (R_group / R_fold)^2 of the rays that reach the fold", R_fold being the
+    // ball around every bounded operand.
     void emit_compact_ivl(int idx) {
         const rt_node& n = d_.nodes[idx];
-        if (n.kind == RT_NODE_CSG) {
-            emit_compact_ivl(n.a);
-            emit_compact_ivl(n.b);
-            DevOp& o = op(OP_CSG, idx, 0);
-            o.csg_op = n.op;
-            --idepth_;
+        if (n.kind != RT_NODE_CSG) {
+            op(OP_LEAF_IVL, idx, 0);
+            ivl_push();
             return;
         }
-        op(OP_LEAF_IVL, idx, 0);
-        ivl_push();
+        std::vector<int> spine, rhs;   // fold steps, innermost first
+        int cur = idx;
+        while (d_.nodes[cur].kind == RT_NODE_CSG && d_.nodes[cur].op == n.op) {
+            spine.push_back(cur);
+            rhs.push_back(d_.nodes[cur].b);
+            cur = d_.nodes[cur].a;
+        }
+        std::reverse(spine.begin(), spine.end());
+        std::reverse(rhs.begin(), rhs.end());
+        emit_compact_ivl(cur);
+
+        const size_t m = rhs.size();
+        std::vector<char> ball_leaf(m);
+        Bound fold;
+        fold.kind = Bound::Empty;
+        {
+            const Bound b0 = bound(cur);
+            if (b0.kind == Bound::Ball) fold = b0;
+        }
+        for (size_t k = 0; k < m; ++k) {
+            const int kind = d_.nodes[rhs[k]].kind;
+            ball_leaf[k] = kind == RT_NODE_SPHERE || kind == RT_NODE_POKEBALL;
+            const Bound b = bound(rhs[k]);
+            if (b.kind == Bound::Ball) fold = merge_union(fold, b);
+        }
+        // best[k] = cost of operands [0, k); from[k] = start of the last run
+        constexpr size_t kMaxRun = 32;
+        std::vector<double> best(m + 1, 0.0);
+        std::vector<size_t> from(m + 1, 0);
+        for (size_t k = 1; k <= m; ++k) {
+            best[k] = best[k - 1] + 1.0;
+            from[k] = k - 1;
+            if (!ball_leaf[k - 1] || fold.kind != Bound::Ball || fold.r <= 0.0) continue;
+            Bound g = bound(rhs[k - 1]);
+            for (size_t i = k - 1; i-- > 0 && k - i <= kMaxRun;) {
+                if (!ball_leaf[i]) break;
+                g = merge_union(g, bound(rhs[i]));
+                const double f = std::min(1.0, g.r / fold.r);
+                const double c = best[i] + 1.0 + f * f * (double)(k - i);
+                if (c < best[k]) {
+                    best[k] = c;
+                    from[k] = i;
+                }
+            }
+        }
+        std::vector<std::pair<size_t, size_t>> runs;
+        for (size_t k = m; k > 0; k = from[k]) runs.emplace_back(from[k], k);
+        std::reverse(runs.begin(), runs.end());
+        for (const auto& run : runs) {
+            const size_t i = run.first, j = run.second;
+            if (j - i >= 2) {
+                Bound g = bound(rhs[i]);
+                for (size_t k = i + 1; k < j; ++k) g = merge_union(g, bound(rhs[k]));
+                DevOp& h = op(OP_IVL_GROUP, (int)(gb_->size() / 4), 2 * (int)(j - i));
+                h.csg_op = n.op;
+                const double mag = std::fabs(g.c[0]) + std::fabs(g.c[1]) + std::fabs(g.c[2]) + g.r;
+                gb_->push_back(g.c[0]);
+                gb_->push_back(g.c[1]);
+                gb_->push_back(g.c[2]);
+                gb_->push_back(g.r * (1.0 + 1e-7) + 1e-7 * (1.0 + mag));
+            }
+            for (size_t k = i; k < j; ++k) {
+                emit_compact_ivl(rhs[k]);
+                DevOp& o = op(OP_CSG, spine[k], 0);
+                o.csg_op = n.op;
+                --idepth_;
+            }
+        }
     }
 
     CompiledScene run() {
         CompiledScene cs;
         ops_ = &cs.ops;
+        gb_ = &cs.gbounds;
         for (int k = 0; k < d_.n_nodes; ++k)
             if (d_.nodes[k].kind == RT_NODE_POKEBALL) cs.has_pokeball = true;
         for (int i = 0; i < d_.n_objects; ++i) {
@@ -310,6 +387,7 @@ public:
 private:
     const rt_scene_desc& d_;
     std::vector<DevOp>* ops_ = nullptr;
+    std::vector<double>* gb_ = nullptr;
     int rdepth_ = 0, idepth_ = 0, max_r_ = 0, max_i_ = 0;
 
     DevOp& op(int code, int node, int top) {

@@ -41,7 +41,9 @@ enum DevOpCode : int32_t {
     OP_LEAF_ISECT = 4,  // hit = Primitive::intersect(leaf, current ray, range)
     OP_CSG_ISECT = 5,   // hit = CSG::intersect from top interval, range
     OP_XPOP_HIT = 6,    // (eager) map hit back through transform node, check range, pop ray
-    OP_NEVER = 7        // the subtree can never hit (degenerate Scaling, transform.cpp:97)
+    OP_NEVER = 7,       // the subtree can never hit (degenerate Scaling, transform.cpp:97)
+    OP_IVL_GROUP = 8    // compact: the next `top` ops fold sphere leaves into the stack top with csg_op;
+                        // skipped (one combine with an empty interval) when no lane's line meets bound `node`
 };
 
 struct DevObj {
@@ -68,6 +70,7 @@ struct DevOp {
 struct CompiledScene {
     std::vector<DevObj> objs;
     std::vector<DevOp> ops;
+    std::vector<double> gbounds;   // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame
     int max_ray_depth = 0;   // transform nesting on any path
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter

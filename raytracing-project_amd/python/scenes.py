@@ -232,6 +232,50 @@ def torture_scenes(dpi: int = 24) -> dict[str, dict]:
         {"intersection": [s_poke,
                           {"sphere": {"position": [0.0, 0.9, -2.5], "radius": 0.7, "color": _mat([0.9, 0.6, 0.2])}}]},
     ], dpi=dpi)
+    def _cluster(cx, cy, cz, r, n, col, spread=0.18):
+        out = []
+        for i in range(n):
+            a = 2.399963 * i
+            out.append({"sphere": {"position": [cx + spread * math.cos(a), cy + spread * math.sin(a), cz + 0.05 * i],
+                                   "radius": r * (1.0 - 0.08 * i), "color": _mat(col)}})
+        return out
+    # n-ary folds with runs of small spheres: OP_IVL_GROUP culling inside the
+    # CSG program (scene_compile.cpp emit_compact_ivl) for all three operators
+    sc["csg_groups"] = _base([
+        floor,
+        {"translation": {"factors": [-1.3, 0.1, -0.5], "subject": {"union": [
+            {"sphere": {"position": [0, 0, -1], "radius": 0.7, "color": _mat([0.2, 0.5, 0.5])}},
+            *_cluster(0.0, 0.75, -0.8, 0.12, 5, [0.9, 0.9, 0.9]),
+            {"pokeball": {"position": [0.6, -0.5, -0.7], "radius": 0.2, "button_dir": [0, 0, 1]}},
+            *_cluster(-0.6, -0.4, -0.6, 0.08, 4, [0.3, 0.2, 0.1], spread=0.1),
+            {"halfSpace": {"position": [0, -0.55, 0], "normal": [0, -1, 0], "color": _mat([0.5, 0.5, 0.5])}},
+            *_cluster(0.5, 0.4, -0.5, 0.1, 3, [0.8, 0.2, 0.2], spread=0.12)]}}},
+        {"difference": [
+            {"sphere": {"position": [1.2, 0.1, -1.2], "radius": 0.8, "color": _mat([0.8, 0.7, 0.3])}},
+            *_cluster(1.2, 0.1, -0.45, 0.22, 6, [0.2, 0.2, 0.8], spread=0.35),
+            *_cluster(1.7, 0.6, -1.0, 0.15, 3, [0.2, 0.8, 0.2], spread=0.1)]},
+        {"intersection": [
+            {"sphere": {"position": [0.0, -0.6, -0.4], "radius": 0.45, "color": _mat([0.7, 0.3, 0.7])}},
+            {"sphere": {"position": [0.15, -0.5, -0.4], "radius": 0.45, "color": _mat([0.3, 0.7, 0.7])}},
+            {"sphere": {"position": [-0.1, -0.45, -0.35], "radius": 0.4, "color": _mat([0.7, 0.7, 0.3])}},
+            {"sphere": {"position": [0.05, -0.7, -0.45], "radius": 0.42, "color": _mat([0.5, 0.5, 0.5])}}]},
+    ], dpi=dpi)
+    sc["csg_groups_inside"] = {
+        # eye inside an n-ary union whose later operands are grouped
+        "screen": {"dpi": dpi, "dimensions": [4, 3], "position": [-2, -1.5, 0], "observer": [0, 0, 1]},
+        "medium": {"ambient": [0.3, 0.3, 0.3], "index": 1.0, "recursion": 2},
+        "background": [0.1, 0.1, 0.1],
+        "sources": [{"position": [0, 0.5, 0.5], "intensity": [5, 5, 5]}],
+        "objects": [
+            {"union": [
+                {"sphere": {"position": [0, 0, 1], "radius": 3.0, "color": _mat([0.6, 0.5, 0.4])}},
+                *_cluster(0.3, 0.2, -1.5, 0.25, 5, [0.2, 0.5, 0.9], spread=0.4),
+                *_cluster(-1.0, -0.6, -1.0, 0.2, 3, [0.9, 0.5, 0.2], spread=0.2)]},
+            {"difference": [
+                {"sphere": {"position": [0, 0, 1], "radius": 2.5, "color": _mat([0.4, 0.6, 0.4])}},
+                *_cluster(0.0, 0.0, 1.0, 0.3, 4, [0.9, 0.9, 0.2], spread=0.2)]},
+        ],
+    }
     sc["recursion0"] = copy.deepcopy(sc["reflect_refract"])
     sc["recursion0"]["medium"]["recursion"] = 0
     sc["inside_camera"] = {

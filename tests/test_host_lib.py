@@ -83,6 +83,33 @@ def test_mt19937_jump_polynomials_cpu():
     assert amd.rt_test_mt_jump_cpu(3, 5) == 0   # non power-of-two segment length
 
 
+def _compile_info(rt, text):
+    amd = rt.amd_lib()
+    amd.rt_test_compile_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+    sc = rt.load_scene_from_json_text(text)
+    out = (C.c_int32 * 8)()
+    assert amd.rt_test_compile_info(sc.handle, out) == 0
+    keys = ("objects", "obj_groups", "obj_group_members", "ops", "ivl_groups", "ivl_group_members",
+            "has_eager", "max_ivl_depth")
+    return dict(zip(keys, out))
+
+
+def test_compiled_cull_groups(rt):
+    """Host compile of the device object table: object cull headers and CSG
+    operand groups (scene_compile.cpp) appear where the bench scene needs
+    them and never in scenes without n-ary folds of spheres."""
+    import scenes
+    cfg4 = _compile_info(rt, scenes.config_json(4, dpi=8)[0])
+    # 15 objects + 2 headers; the 20-sphere union gets operand groups
+    assert cfg4["objects"] == 17 and cfg4["obj_groups"] == 2
+    assert cfg4["ivl_groups"] >= 3 and cfg4["ivl_group_members"] >= 10
+    tort = scenes.torture_scenes(dpi=8)
+    g = _compile_info(rt, json.dumps(tort["csg_groups"]))
+    assert g["ivl_groups"] >= 3
+    assert _compile_info(rt, json.dumps(tort["reflect_refract"]))["ivl_groups"] == 0
+    assert _compile_info(rt, json.dumps(tort["xform_in_csg"]))["has_eager"] == 1
+
+
 def test_cli_usage_and_load_errors(tmp_path):
     r = subprocess.run([RAY], capture_output=True, text=True)
     assert r.returncode == 1 and "Usage:" in r.stderr and "--paper" in r.stderr
