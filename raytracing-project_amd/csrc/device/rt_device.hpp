@@ -106,7 +106,7 @@ struct DevScene {
     const rt_light* lights;
     const DevObj* objs;
     const DevOp* ops;
-    const double* gb;   // OP_IVL_GROUP bounds (cx, cy, cz, r)
+    const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
     int n_lights, n_objs;
     int cam_nx, cam_ny;
     int rec_limit, cull;
@@ -794,19 +794,38 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
     R.c1 = (exitE == 0 ? A.c0 : exitE == 1 ? A.c1 : exitE == 2 ? B.c0 : B.c1) | (flipX ? REF_FLIP : 0);
 }
 
-// Can the full line of r meet the ball g = (cx, cy, cz, r)?  Conservative:
-// a lane answering "no" gets an empty Primitive::interval from every sphere
-// inside g (the radius is inflated and the disc test has an absolute margin
-// well above its rounding error).
-__device__ __forceinline__ bool line_touch(const double* g, const DRay& r) {
-    const V3 oc = v3(r.o.x - g[0], r.o.y - g[1], r.o.z - g[2]);
-    const double b = dot3(oc, r.d);
-    const double c2 = dot3(oc, oc);
-    const double disc = b * b - (c2 - g[3] * g[3]);
-    return !(disc < -(1e-9 * c2 + 1e-12));
+// ------------------------------------------------------------ f32 culling
+// Cull tests run in float (full-rate VALU; the trace itself is FP64).  They
+// are conservative: "false" only when the segment [t0, t1] of the ray stays
+// farther than r from the ball's centre even after the float rounding of
+// every input and operation (the host grows each ball by 1e-6 of its scale,
+// float_ball() in scene_compile.cpp; the test adds 4e-6 of the magnitudes it
+// works with).  NaN rays always pass.  Culling therefore never changes a
+// result, only skips work no lane needs.
+constexpr float RT_INF_F = __builtin_inff();
+
+struct FRay {
+    float ox, oy, oz, dx, dy, dz;
+};
+
+__device__ __forceinline__ FRay to_fray(const DRay& r) {
+    return FRay{(float)r.o.x, (float)r.o.y, (float)r.o.z, (float)r.d.x, (float)r.d.y, (float)r.d.z};
 }
 
-// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
+__device__ __forceinline__ bool ball_touch(const float* g, const FRay& r, float t0, float t1) {
+    const float ox = r.ox - g[0], oy = r.oy - g[1], oz = r.oz - g[2];
+    const float b = ox * r.dx + oy * r.dy + oz * r.dz;
+    const float t = __builtin_fminf(__builtin_fmaxf(-b, t0), t1);   // closest point of the segment
+    const float qx = __builtin_fmaf(t, r.dx, ox);
+    const float qy = __builtin_fmaf(t, r.dy, oy);
+    const float qz = __builtin_fmaf(t, r.dz, oz);
+    const float q2 = qx * qx + qy * qy + qz * qz;
+    const float e = 4e-6f * (__builtin_fabsf(ox) + __builtin_fabsf(oy) + __builtin_fabsf(oz) + __builtin_fabsf(t) + g[3]);
+    const float R = g[3] + e;
+    return !(q2 > R * R);
+}
+
+// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
 // The top two stack entries are plain locals (VGPRs); only trees that are
 // not left-deep folds touch the spill array (scratch), at uniform indices.
 template <bool DEEP, class CT>
@@ -819,6 +838,7 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
     double sp_t0[NSP], sp_t1[NSP], sp_s0[NSP], sp_s1[NSP];
     int sp_ok[NSP], sp_c0[NSP], sp_c1[NSP];
     int sp = 0;   // stack entries (wave-uniform)
+    const FRay fr = to_fray(r);
     for (int pc = pc0; pc < pc1; ++pc) {
         const DevOp op = S.ops[pc];
         if (op.op == rtamd::OP_LEAF_IVL) {
@@ -833,7 +853,8 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
             tos = v;
             ++sp;
         } else if (op.op == rtamd::OP_IVL_GROUP) {
-            if (S.cull && !__any(line_touch(S.gb + 4 * op.node, r))) {
+            // the full line: Primitive::interval has no range
+            if (S.cull && !__any(ball_touch(S.gb + 4 * op.node, fr, -RT_INF_F, RT_INF_F))) {
                 cnt.inc(RT_OPC_CULLED);
                 CIvl e, v;
                 e.ok = 0;
@@ -1014,20 +1035,6 @@ __device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DR
     }
 }
 
-// Conservative test: can the ray's [tmin,tmax] segment touch the bound?
-__device__ __forceinline__ bool bound_touch(const DevObj& ob, const DRay& r, double tmin, double tmax) {
-    V3 oc = v3(r.o.x - ob.bc[0], r.o.y - ob.bc[1], r.o.z - ob.bc[2]);
-    const double b = dot3(oc, r.d);
-    const double c = dot3(oc, oc) - ob.br * ob.br;
-    const double disc = b * b - c;
-    if (disc < 0.0) return false;
-    const double s = __builtin_sqrt(disc);
-    const double t0 = -b - s, t1 = -b + s;
-    const double m0 = 1e-6 * (1.0 + __builtin_fabs(tmin));
-    const double m1 = 1e-6 * (1.0 + __builtin_fabs(tmax));
-    return !(t1 < tmin - m0) && !(t0 > tmax + m1);
-}
-
 // Scene::intersect (scene.cpp:10-24): closest hit; every object applies its
 // own accept rule with tmax = closest-so-far, so ties resolve as in the
 // reference (Sphere/HalfSpace accept t == tmax, CSG/transforms do not).
@@ -1039,22 +1046,20 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
     V3 wp = v3(0.0, 0.0, 0.0);
     double wts = 0.0;
     int wcode = 0;
+    const FRay fr = to_fray(r);
+    const float ftmin = (float)tmin;
     for (int o = 0; o < S.n_objs; ++o) {
         const DevObj ob = S.objs[o];
         if (ob.kind == rtamd::OBJ_NEVER) continue;
-        if (ob.kind == rtamd::OBJ_GROUP) {
-            if (S.cull && !__any(bound_touch(ob, r, tmin, closest))) {
+        if (ob.has_bound && S.cull) {
+            // groups skip their members; every bounded object is pre-tested
+            if (!__any(ball_touch(ob.fb, fr, ftmin, (float)closest))) {
                 cnt.inc(RT_OPC_CULLED);
-                o += ob.m;
-            }
-            continue;
-        }
-        if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound && S.cull) {
-            if (!__any(bound_touch(ob, r, tmin, closest))) {
-                cnt.inc(RT_OPC_CULLED);
+                if (ob.kind == rtamd::OBJ_GROUP) o += ob.m;
                 continue;
             }
         }
+        if (ob.kind == rtamd::OBJ_GROUP) continue;
         double t = 0.0, ts = 0.0;
         V3 p;
         int code = 0;
@@ -1076,23 +1081,20 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
 template <bool EAGER, bool DEEP, class CT>
 __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, double tmax, CT& cnt) {
     bool hit = false;
+    const FRay fr = to_fray(r);
+    const float ftmin = (float)tmin, ftmax = (float)tmax;
     for (int o = 0; o < S.n_objs; ++o) {
         if (__all(hit)) break;
         const DevObj ob = S.objs[o];
         if (ob.kind == rtamd::OBJ_NEVER) continue;
-        if (ob.kind == rtamd::OBJ_GROUP) {
-            if (S.cull && !__any(!hit && bound_touch(ob, r, tmin, tmax))) {
+        if (ob.has_bound && S.cull) {
+            if (!__any(!hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
                 cnt.inc(RT_OPC_CULLED);
-                o += ob.m;
-            }
-            continue;
-        }
-        if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound && S.cull) {
-            if (!__any(!hit && bound_touch(ob, r, tmin, tmax))) {
-                cnt.inc(RT_OPC_CULLED);
+                if (ob.kind == rtamd::OBJ_GROUP) o += ob.m;
                 continue;
             }
         }
+        if (ob.kind == rtamd::OBJ_GROUP) continue;
         if (!hit) {
             double t = 0.0, ts = 0.0;
             V3 p;
@@ -1114,45 +1116,71 @@ template <bool EAGER, bool DEEP, class CT>
 __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
     if (hit.mat < 0) return v3(1.0, 0.0, 1.0);
     cnt.inc(RT_OPC_SHADE_CALL);
-    const rt_material* m = &S.mats[hit.mat];
     const V3 n = hit.n;
-    V3 E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
     const double eps = dmax(1e-3, 1e-4 * ht);
-    const double kd = m->kd, ks = m->ks, shin = m->shininess;
-    const V3 alb = ld3(m->albedo);
-    for (int li = 0; li < S.n_lights; ++li) {
-        const rt_light* L = &S.lights[li];
-        cnt.inc(RT_OPC_LIGHT_EVAL);
-        V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
-        double d2 = dot3(tl, tl);
-        if (d2 <= 0.01) d2 = 0.01;
-        const double dist = __builtin_sqrt(d2);
-        const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
-        const double ndotl = dmax(0.0, dot3(n, wi));
-        if (ndotl <= 0.0) continue;
-        const double max_t = dist - eps;
-        if (max_t <= eps) continue;
-        const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
-        const DRay sr = make_ray(so, wi);
-        ++n_occl;
-        if (scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt)) continue;
-        cnt.inc(RT_OPC_SHADE_LIGHT);
-        const double ed = dmax(0.5, dist);
-        const double falloff = 1.0 / (ed * ed);
-        const double f2 = falloff * 2.0;
-        const V3 IL = v3(L->intensity[0] * f2, L->intensity[1] * f2, L->intensity[2] * f2);
-        const double sd = kd * ndotl * 1.5;
-        const V3 Ed = v3(alb.x * IL.x * sd, alb.y * IL.y * sd, alb.z * IL.z * sd);
-        V3 Es = v3(0.0, 0.0, 0.0);
-        if (ks > 0.0) {
-            cnt.inc(RT_OPC_SHADE_SPEC);
-            const V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
-                                        2.0 * dot3(n, wi) * n.z - wi.z));
-            const double rdotv = dmax(0.0, dot3(rr, wo));
-            const double spec = pow(rdotv, shin) * ks;
-            Es = v3(IL.x * spec, IL.y * spec, IL.z * spec);
+    // Two passes over the lights so that only (p, n, eps) stay live across
+    // the shadow queries (register pressure): pass 1 decides, per light, the
+    // reference's early-outs and the occlusion query; pass 2 recomputes the
+    // same light geometry (identical operations, identical bits) and
+    // accumulates in the reference's order.  Lights beyond 32 are handled in
+    // further rounds of the same two passes.
+    V3 E = v3(0.0, 0.0, 0.0);
+    {
+        const rt_material* m = &S.mats[hit.mat];
+        E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
+    }
+    for (int l0 = 0; l0 < S.n_lights; l0 += 32) {
+        const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
+        uint32_t lit = 0;
+        for (int li = l0; li < l1; ++li) {
+            const rt_light* L = &S.lights[li];
+            cnt.inc(RT_OPC_LIGHT_EVAL);
+            V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
+            double d2 = dot3(tl, tl);
+            if (d2 <= 0.01) d2 = 0.01;
+            const double dist = __builtin_sqrt(d2);
+            const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
+            const double ndotl = dmax(0.0, dot3(n, wi));
+            if (ndotl <= 0.0) continue;
+            const double max_t = dist - eps;
+            if (max_t <= eps) continue;
+            const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
+            const DRay sr = make_ray(so, wi);
+            ++n_occl;
+            if (scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt)) continue;
+            lit |= 1u << (li - l0);
         }
-        E = combine(E, combine(Ed, Es));
+        if (!lit) continue;
+        const rt_material* m = &S.mats[hit.mat];
+        const double kd = m->kd, ks = m->ks, shin = m->shininess;
+        const V3 alb = ld3(m->albedo);
+        for (int li = l0; li < l1; ++li) {
+            if (!((lit >> (li - l0)) & 1u)) continue;
+            const rt_light* L = &S.lights[li];
+            V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
+            double d2 = dot3(tl, tl);
+            if (d2 <= 0.01) d2 = 0.01;
+            const double dist = __builtin_sqrt(d2);
+            const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
+            const double ndotl = dmax(0.0, dot3(n, wi));
+            cnt.inc(RT_OPC_SHADE_LIGHT);
+            const double ed = dmax(0.5, dist);
+            const double falloff = 1.0 / (ed * ed);
+            const double f2 = falloff * 2.0;
+            const V3 IL = v3(L->intensity[0] * f2, L->intensity[1] * f2, L->intensity[2] * f2);
+            const double sd = kd * ndotl * 1.5;
+            const V3 Ed = v3(alb.x * IL.x * sd, alb.y * IL.y * sd, alb.z * IL.z * sd);
+            V3 Es = v3(0.0, 0.0, 0.0);
+            if (ks > 0.0) {
+                cnt.inc(RT_OPC_SHADE_SPEC);
+                const V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
+                                            2.0 * dot3(n, wi) * n.z - wi.z));
+                const double rdotv = dmax(0.0, dot3(rr, wo));
+                const double spec = pow(rdotv, shin) * ks;
+                Es = v3(IL.x * spec, IL.y * spec, IL.z * spec);
+            }
+            E = combine(E, combine(Ed, Es));
+        }
     }
     E.x = dmin(1.5, E.x);
     E.y = dmin(1.5, E.y);

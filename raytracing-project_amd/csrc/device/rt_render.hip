@@ -75,8 +75,17 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
     }
 }
 
+#ifndef RT_K_STD_WAVES
+#define RT_K_STD_WAVES 0
+#endif
+#if RT_K_STD_WAVES > 0
+#define RT_K_STD_ATTR __attribute__((amdgpu_waves_per_eu(RT_K_STD_WAVES, RT_K_STD_WAVES)))
+#else
+#define RT_K_STD_ATTR
+#endif
+
 template <bool E, bool D, bool SEC, bool C>
-__global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
+__global__ __launch_bounds__(256) RT_K_STD_ATTR void k_std(DevScene S, StdParams P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int s = lane & 7;
@@ -415,7 +424,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     S.lights = ws.lights.as<rt_light>();
     S.objs = ws.objs.as<DevObj>();
     S.ops = ws.ops.as<DevOp>();
-    S.gb = ws.gb.as<double>();
+    S.gb = ws.gb.as<float>();
     S.n_lights = d.n_lights;
     S.n_objs = (int)cs.objs.size();
     S.cam_nx = rt_camera_width(&d.camera);

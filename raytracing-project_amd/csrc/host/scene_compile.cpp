@@ -50,6 +50,15 @@ Bound merge_union(const Bound& a, const Bound& b) {
     return o;
 }
 
+// A ball in float for the device's f32 cull tests (rt_device.hpp ball_touch):
+// the double ball grown by 1e-6 of its scale, rounded outward, so that the
+// float centre's rounding error stays inside it.
+void float_ball(const double c[3], double r, float out[4]) {
+    const double mag = std::fabs(c[0]) + std::fabs(c[1]) + std::fabs(c[2]) + r;
+    for (int k = 0; k < 3; ++k) out[k] = (float)c[k];
+    out[3] = std::nextafter((float)(r + 1e-6 * (1.0 + mag)), INFINITY);
+}
+
 bool is_degenerate_scaling(const rt_node& n) {
     const double kEPS = 1e-6;   // core.h:10, checked at transform.cpp:97
     return n.kind == RT_NODE_SCALING &&
@@ -234,40 +243,45 @@ public:
             if (b.kind == Bound::Ball) fold = merge_union(fold, b);
         }
         // best[k] = cost of operands [0, k); from[k] = start of the last run
+        // (a header is an f32 line test, ~1/4 of an FP64 sphere interval)
         constexpr size_t kMaxRun = 32;
+        constexpr double kHeader = 0.25;
         std::vector<double> best(m + 1, 0.0);
         std::vector<size_t> from(m + 1, 0);
+        std::vector<char> hdr(m + 1, 0), grouped(m + 1, 0);
         for (size_t k = 1; k <= m; ++k) {
             best[k] = best[k - 1] + 1.0;
             from[k] = k - 1;
             if (!ball_leaf[k - 1] || fold.kind != Bound::Ball || fold.r <= 0.0) continue;
             Bound g = bound(rhs[k - 1]);
-            for (size_t i = k - 1; i-- > 0 && k - i <= kMaxRun;) {
+            for (size_t i = k; i-- > 0 && k - i <= kMaxRun;) {
                 if (!ball_leaf[i]) break;
-                g = merge_union(g, bound(rhs[i]));
+                if (i + 1 < k) g = merge_union(g, bound(rhs[i]));
                 const double f = std::min(1.0, g.r / fold.r);
-                const double c = best[i] + 1.0 + f * f * (double)(k - i);
+                const double c = best[i] + kHeader + f * f * (double)(k - i);
                 if (c < best[k]) {
                     best[k] = c;
                     from[k] = i;
+                    hdr[k] = 1;
                 }
             }
         }
         std::vector<std::pair<size_t, size_t>> runs;
-        for (size_t k = m; k > 0; k = from[k]) runs.emplace_back(from[k], k);
+        for (size_t k = m; k > 0; k = from[k]) {
+            runs.emplace_back(from[k], k);
+            if (hdr[k]) grouped[from[k]] = 1;
+        }
         std::reverse(runs.begin(), runs.end());
         for (const auto& run : runs) {
             const size_t i = run.first, j = run.second;
-            if (j - i >= 2) {
+            if (j - i >= 2 || grouped[i]) {
                 Bound g = bound(rhs[i]);
                 for (size_t k = i + 1; k < j; ++k) g = merge_union(g, bound(rhs[k]));
                 DevOp& h = op(OP_IVL_GROUP, (int)(gb_->size() / 4), 2 * (int)(j - i));
                 h.csg_op = n.op;
-                const double mag = std::fabs(g.c[0]) + std::fabs(g.c[1]) + std::fabs(g.c[2]) + g.r;
-                gb_->push_back(g.c[0]);
-                gb_->push_back(g.c[1]);
-                gb_->push_back(g.c[2]);
-                gb_->push_back(g.r * (1.0 + 1e-7) + 1e-7 * (1.0 + mag));
+                float fb[4];
+                float_ball(g.c, g.r, fb);
+                gb_->insert(gb_->end(), fb, fb + 4);
             }
             for (size_t k = i; k < j; ++k) {
                 emit_compact_ivl(rhs[k]);
@@ -337,6 +351,7 @@ public:
                 double mag = std::fabs(b.c[0]) + std::fabs(b.c[1]) + std::fabs(b.c[2]) + b.r;
                 for (int k = 0; k < 3; ++k) o.bc[k] = b.c[k];
                 o.br = b.r * (1.0 + 1e-7) + 1e-7 * (1.0 + mag);
+                float_ball(b.c, b.r, o.fb);
             }
             cs.objs.push_back(o);
         }
@@ -376,6 +391,7 @@ public:
                 const double mag = std::fabs(g.c[0]) + std::fabs(g.c[1]) + std::fabs(g.c[2]) + g.r;
                 for (int k = 0; k < 3; ++k) h.bc[k] = g.c[k];
                 h.br = g.r * (1.0 + 1e-7) + 1e-7 * (1.0 + mag);
+                float_ball(g.c, g.r, h.fb);
                 out.push_back(h);
             }
             for (size_t k = i; k < j; ++k) out.push_back(in[k]);
@@ -387,7 +403,7 @@ public:
 private:
     const rt_scene_desc& d_;
     std::vector<DevOp>* ops_ = nullptr;
-    std::vector<double>* gb_ = nullptr;
+    std::vector<float>* gb_ = nullptr;
     int rdepth_ = 0, idepth_ = 0, max_r_ = 0, max_i_ = 0;
 
     DevOp& op(int code, int node, int top) {

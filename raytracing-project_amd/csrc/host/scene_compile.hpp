@@ -43,7 +43,7 @@ enum DevOpCode : int32_t {
     OP_XPOP_HIT = 6,    // (eager) map hit back through transform node, check range, pop ray
     OP_NEVER = 7,       // the subtree can never hit (degenerate Scaling, transform.cpp:97)
     OP_IVL_GROUP = 8    // compact: the next `top` ops fold sphere leaves into the stack top with csg_op;
-                        // skipped (one combine with an empty interval) when no lane's line meets bound `node`
+                        // skipped (one combine with an empty interval) when no lane's line meets ball `node`
 };
 
 struct DevObj {
@@ -58,6 +58,7 @@ struct DevObj {
     int32_t pad;
     double bc[3];       // bound centre
     double br;          // bound radius (already inflated)
+    float fb[4];        // the same ball in float (cx, cy, cz, r), inflated for the f32 cull test
 };
 
 struct DevOp {
@@ -70,7 +71,7 @@ struct DevOp {
 struct CompiledScene {
     std::vector<DevObj> objs;
     std::vector<DevOp> ops;
-    std::vector<double> gbounds;   // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame
+    std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated
     int max_ray_depth = 0;   // transform nesting on any path
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter

@@ -136,7 +136,8 @@ def amd_lib():
     global _amd
     if _amd is None:
         host_lib()
-        lib = _load(os.path.join(LIB_DIR, "librtamd.so"))
+        # RTAMD_LIB: diagnostic override (tools/ build experiments); never a fallback
+        lib = _load(os.environ.get("RTAMD_LIB") or os.path.join(LIB_DIR, "librtamd.so"))
         lib.rt_render.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, C.POINTER(Stats)]
         lib.rt_render_rows_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                               C.POINTER(C.c_int32), C.c_int, C.c_void_p, C.c_void_p,

@@ -97,7 +97,7 @@ def _compile_info(rt, text):
 def test_compiled_cull_groups(rt):
     """Host compile of the device object table: object cull headers and CSG
     operand groups (scene_compile.cpp) appear where the bench scene needs
-    them and never in scenes without n-ary folds of spheres."""
+    them and never in scenes without CSG."""
     import scenes
     cfg4 = _compile_info(rt, scenes.config_json(4, dpi=8)[0])
     # 15 objects + 2 headers; the 20-sphere union gets operand groups
@@ -106,7 +106,7 @@ def test_compiled_cull_groups(rt):
     tort = scenes.torture_scenes(dpi=8)
     g = _compile_info(rt, json.dumps(tort["csg_groups"]))
     assert g["ivl_groups"] >= 3
-    assert _compile_info(rt, json.dumps(tort["reflect_refract"]))["ivl_groups"] == 0
+    assert _compile_info(rt, json.dumps(tort["rotation_scaling"]))["ivl_groups"] == 0
     assert _compile_info(rt, json.dumps(tort["xform_in_csg"]))["has_eager"] == 1
 
 
