@@ -75,17 +75,16 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
     }
 }
 
-#ifndef RT_K_STD_WAVES
-#define RT_K_STD_WAVES 0
-#endif
-#if RT_K_STD_WAVES > 0
-#define RT_K_STD_ATTR __attribute__((amdgpu_waves_per_eu(RT_K_STD_WAVES, RT_K_STD_WAVES)))
-#else
-#define RT_K_STD_ATTR
+// Occupancy target of the lean variants (E = D = SEC = false): 4 waves/SIMD
+// caps them at 128 VGPRs; the few values the compiler then spills are
+// long-lived (stored once, reloaded once), and the extra wave per SIMD hides
+// FP64 latency (measured 21.6 -> 19.2 ms on config 4; 5 and 6 are slower).
+#ifndef RT_LEAN_WAVES
+#define RT_LEAN_WAVES 4
 #endif
 
 template <bool E, bool D, bool SEC, bool C>
-__global__ __launch_bounds__(256) RT_K_STD_ATTR void k_std(DevScene S, StdParams P) {
+__device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int s = lane & 7;
@@ -125,6 +124,17 @@ __global__ __launch_bounds__(256) RT_K_STD_ATTR void k_std(DevScene S, StdParams
     flush_counters(P.counters, ni, no, cnt);
 }
 
+template <bool E, bool D, bool SEC, bool C>
+__global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
+    std_body<E, D, SEC, C>(S, P);
+}
+
+template <bool C>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
+                                                                                                       StdParams P) {
+    std_body<false, false, false, C>(S, P);
+}
+
 struct PaperParams {
     int W, H;
     int n_ext;
@@ -145,7 +155,7 @@ struct PaperParams {
 };
 
 template <bool E, bool D, bool C>
-__global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
+__device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -176,6 +186,17 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
         }
     }
     flush_counters(P.counters, ni, no, cnt);
+}
+
+template <bool E, bool D, bool C>
+__global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
+    paper_primary_body<E, D, C>(S, P);
+}
+
+template <bool C>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
+    DevScene S, PaperParams P) {
+    paper_primary_body<false, false, C>(S, P);
 }
 
 // apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
@@ -292,7 +313,8 @@ void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, con
         else launch_std_c<false, true, false>(c, grid, st, S, P);
     } else {
         if (sec) launch_std_c<false, false, true>(c, grid, st, S, P);
-        else launch_std_c<false, false, false>(c, grid, st, S, P);
+        else if (c) hipLaunchKernelGGL((k_std_lean<true>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_std_lean<false>), grid, dim3(256), 0, st, S, P);
     }
 }
 template <bool E, bool D>
@@ -303,7 +325,8 @@ void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const 
 void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
     if (e) launch_paper_c<true, true>(c, grid, st, S, P);
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
-    else launch_paper_c<false, false>(c, grid, st, S, P);
+    else if (c) hipLaunchKernelGGL((k_paper_primary_lean<true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary_lean<false>), grid, dim3(256), 0, st, S, P);
 }
 
 // ------------------------------------------------------------ host side
