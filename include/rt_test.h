@@ -12,9 +12,10 @@ extern "C" {
 #endif
 
 /* CPU check of the GF(2) jump polynomials (csrc/host/mt_poly.cpp): for
- * levels j < levels, applying x^(624*K*2^j) mod phi to the first window must
- * equal advancing it K*2^j twist blocks sequentially.  Returns the number of
- * mismatching levels (0 = all good), -1 on error. */
+ * tree levels j < levels and m = 1..7, applying x^(624*K*m*8^j) mod phi to
+ * the seed window must equal advancing it m*8^j*K twist blocks
+ * sequentially.  Returns the number of mismatching polynomials (0 = all
+ * good), -1 on error. */
 int rt_test_mt_jump_cpu(int K_blocks, int levels);
 
 /* GPU: generate the jitter stream for output indices [q0, q1) (even) with the

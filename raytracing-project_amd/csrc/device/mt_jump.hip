@@ -3,27 +3,35 @@
 // The reference consumes ONE serial std::mt19937(12345) stream through
 // uniform_real_distribution<double>(-0.5,0.5) (raytracer/src/tracer.cpp:
 // 284-293; libstdc++ generate_canonical, random.tcc:3348-3378).  Here the
-// stream is cut into segments of K twist blocks.  Kernel 1 jumps the
-// generator to every segment start (GF(2) jump polynomials from
-// csrc/host/mt_poly.cpp: window' = XOR_i p_i * window shifted by i); kernel 2
-// regenerates each segment sequentially inside one workgroup (the twist is
-// split into its three dependent phases of 227/227/170 words) and writes the
-// jitter doubles.  Output: jit[(q - q0)/2] = uniform(w_q, w_{q+1}) for every
-// even output index q in [q0, q1).
+// stream is cut into segments of K twist blocks.  k_mt_jump computes the
+// window at every segment start with a radix-8 tree of GF(2) jumps
+// (csrc/host/mt_poly.cpp: window' = XOR_i p_i * window shifted by i), each
+// jump split over S workgroups by tap ranges; k_mt_fill regenerates every
+// segment inside one workgroup and writes the jitter doubles.  Output:
+// jit[(q - q0)/2] = uniform(w_q, w_{q+1}) for every even output index q in
+// [q0, q1).
+//
+// Twist with one barrier per block: thread t < 227 owns words t, 227+t and
+// 454+t of the new block.  Word 227+t reads new word t through the +397 tap
+// and word 454+t reads new word 227+t, so both come from the same thread's
+// registers; only word 623 needs new word 0 (its +1 neighbour), which
+// thread 169 recomputes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
 
 #include "mt_jump.hpp"
+#include "mt_poly.hpp"
 
 namespace {
 
 constexpr int N = 624;
 constexpr int DEG = 19937;
-constexpr int JUMP_BUF = DEG + N;           // raw words w_n .. w_{n+DEG+N-1}
-constexpr int JUMP_THREADS = 640;
-constexpr int FILL_THREADS = 320;
+constexpr int JUMP_BUF = DEG + N;   // raw words w_n .. w_{n+DEG+N-1}
+constexpr int JUMP_THREADS = 320;   // 312 correlation lanes x 2 outputs
+constexpr int FILL_THREADS = 256;
+constexpr int MAX_LEVELS = 8;
 
 __device__ __forceinline__ uint32_t twist_word(uint32_t wk, uint32_t wk1, uint32_t wk397) {
     const uint32_t y = (wk & 0x80000000u) | (wk1 & 0x7fffffffu);
@@ -49,134 +57,239 @@ __device__ __forceinline__ double jitter_from(uint32_t w0, uint32_t w1) {
     return (ret * (0.5 - -0.5)) + -0.5;
 }
 
-// Generate buf[N .. N + 624*nblocks) from the window in buf[0..N) with the
-// three-phase twist (phase 2 reads phase-1 outputs through the +397 tap).
-__device__ __forceinline__ void twist_blocks(uint32_t* buf, int nblocks, int limit) {
-    for (int b = 0; b < nblocks; ++b) {
-        uint32_t* w = buf + b * N;
-        for (int j = threadIdx.x; j < 227; j += blockDim.x)
-            if (N + b * N + j < limit) w[N + j] = twist_word(w[j], w[j + 1], w[j + 397]);
-        __syncthreads();
-        for (int j = 227 + threadIdx.x; j < 454; j += blockDim.x)
-            if (N + b * N + j < limit) w[N + j] = twist_word(w[j], w[j + 1], w[j + 397]);
-        __syncthreads();
-        for (int j = 454 + threadIdx.x; j < N; j += blockDim.x)
-            if (N + b * N + j < limit) w[N + j] = twist_word(w[j], w[j + 1], w[j + 397]);
-        __syncthreads();
+// One twist block: nw[0..N) from the previous block o[0..N) (disjoint LDS
+// ranges).  Called by every thread; words at index >= lim are not stored.
+__device__ __forceinline__ void twist_block(const uint32_t* o, uint32_t* nw, int lim) {
+    const int t = threadIdx.x;
+    if (t < 227) {
+        const uint32_t n0 = twist_word(o[t], o[t + 1], o[t + 397]);
+        const uint32_t n1 = twist_word(o[227 + t], o[228 + t], n0);
+        if (t < lim) nw[t] = n0;
+        if (227 + t < lim) nw[227 + t] = n1;
+        if (t < 170) {
+            const uint32_t nx = (t == 169) ? twist_word(o[0], o[1], o[397]) : o[455 + t];
+            const uint32_t n2 = twist_word(o[454 + t], nx, n1);
+            if (454 + t < lim) nw[454 + t] = n2;
+        }
     }
 }
 
-// Tree doubling, level j: ckpt[c] = jump(ckpt[c - 2^j]) by x^(624*K*2^j) for
-// c in [lo, lo + gridDim.x).  The jump is the correlation
-// out[j] = XOR_{i in taps} w[i + j] over the raw words regenerated from the
-// source window; taps = exponents with a 1 coefficient (host-built list,
-// staged in LDS as 16-bit offsets and read 8 at a time by broadcast).
+__device__ __forceinline__ int ckpt_parts(int64_t c, const int8_t* parts) {
+    if (c == 0) return 1;
+    const int j = (63 - __builtin_clzll((unsigned long long)c)) / 3;   // c in [8^j, 8^(j+1))
+    return parts[j];
+}
+
+struct JumpArgs {
+    int64_t lo;                 // 8^j: this level computes c in [lo, lo + gridDim.x)
+    int S;                      // partial jumps per checkpoint (gridDim.y)
+    int32_t off[8], len[8];     // tap slice of x^(624*K*m*8^j), m = c / lo
+    int8_t parts[MAX_LEVELS];   // partial count of the checkpoints of every level
+};
+
+// Tree level j: ckpt[c] = jump(ckpt[c - m*lo]) by x^(624*K*m*lo), partial
+// s of S over the taps [s*len/S, (s+1)*len/S).  The jump is the correlation
+// out[k] = XOR_{i in taps} w[i + k] over the raw words regenerated from the
+// source window; taps are staged in LDS as 16-bit exponents and read 8 at a
+// time by broadcast.
 constexpr int MAX_TAPS = DEG + 8;
-__global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump_level(const uint32_t* __restrict__ taps, int ntaps,
-                                                                int64_t lo, int64_t stride,
-                                                                uint32_t* __restrict__ ckpt) {
+__global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint16_t* __restrict__ taps, JumpArgs A,
+                                                          uint32_t* __restrict__ ckpt) {
     __shared__ uint32_t buf[JUMP_BUF + 8];
     __shared__ __attribute__((aligned(16))) uint16_t tp[MAX_TAPS];
-    const int64_t c = lo + blockIdx.x;
+    const int64_t c = A.lo + blockIdx.x;
+    const int s = blockIdx.y;
+    const int m = (int)(c / A.lo);
+    const int64_t r = c - (int64_t)m * A.lo;
     const int tid = threadIdx.x;
-    for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)(c - stride) * N + j];
-    const int n8 = ntaps & ~7;
-    for (int i = tid; i < ntaps; i += blockDim.x) tp[i] = (uint16_t)taps[i];
+    const int np = ckpt_parts(r, A.parts);
+    for (int k = tid; k < N; k += blockDim.x) {
+        uint32_t v = 0;
+        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)r * rtamd::kMTParts + p) * N + k];
+        buf[k] = v;
+    }
+    const int n_all = A.len[m];
+    const int t0 = (int)((int64_t)s * n_all / A.S), t1 = (int)((int64_t)(s + 1) * n_all / A.S);
+    const int ntaps = t1 - t0;
+    const uint16_t* src_taps = taps + A.off[m] + t0;
+    for (int i = tid; i < ntaps; i += blockDim.x) tp[i] = src_taps[i];
     __syncthreads();
-    twist_blocks(buf, (JUMP_BUF - 1) / N, JUMP_BUF);
-    if (tid < N) {
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        const uint32_t* src = buf + tid;
+    for (int b = N; b < JUMP_BUF; b += N) {
+        twist_block(buf + b - N, buf + b, JUMP_BUF - b);
+        __syncthreads();
+    }
+    if (tid < N / 2) {
+        uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+        const uint32_t* sa = buf + tid;
+        const uint32_t* sb = buf + tid + N / 2;
+        const int n8 = ntaps & ~7;
         for (int i = 0; i < n8; i += 8) {
             const uint4 q = *reinterpret_cast<const uint4*>(tp + i);   // uniform address: broadcast
-            a0 ^= src[q.x & 0xffffu];
-            a1 ^= src[q.x >> 16];
-            a2 ^= src[q.y & 0xffffu];
-            a3 ^= src[q.y >> 16];
-            a0 ^= src[q.z & 0xffffu];
-            a1 ^= src[q.z >> 16];
-            a2 ^= src[q.w & 0xffffu];
-            a3 ^= src[q.w >> 16];
+            const uint32_t e0 = q.x & 0xffffu, e1 = q.x >> 16, e2 = q.y & 0xffffu, e3 = q.y >> 16;
+            const uint32_t e4 = q.z & 0xffffu, e5 = q.z >> 16, e6 = q.w & 0xffffu, e7 = q.w >> 16;
+            a0 ^= sa[e0]; b0 ^= sb[e0];
+            a1 ^= sa[e1]; b1 ^= sb[e1];
+            a0 ^= sa[e2]; b0 ^= sb[e2];
+            a1 ^= sa[e3]; b1 ^= sb[e3];
+            a0 ^= sa[e4]; b0 ^= sb[e4];
+            a1 ^= sa[e5]; b1 ^= sb[e5];
+            a0 ^= sa[e6]; b0 ^= sb[e6];
+            a1 ^= sa[e7]; b1 ^= sb[e7];
         }
-        for (int i = n8; i < ntaps; ++i) a0 ^= src[tp[i]];
-        ckpt[(size_t)c * N + tid] = a0 ^ a1 ^ a2 ^ a3;
+        for (int i = n8; i < ntaps; ++i) {
+            a0 ^= sa[tp[i]];
+            b0 ^= sb[tp[i]];
+        }
+        uint32_t* out = ckpt + ((size_t)c * rtamd::kMTParts + s) * N;
+        out[tid] = a0 ^ a1;
+        out[tid + N / 2] = b0 ^ b1;
     }
 }
+
+struct FillArgs {
+    int K;
+    int64_t c0, q0, q1;
+    int8_t parts[MAX_LEVELS];
+};
 
 // One workgroup per segment: regenerate K blocks from the checkpoint and
 // write jitter for outputs in [q0, q1).  buf is a 2-block ring: the block at
-// offset `base` is converted to jitter while the first twist phase of the
-// next block (written at base + 624, mod 1248) runs; no copies.
-__global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __restrict__ ckpt, int K, int64_t c0,
-                                                          int64_t q0, int64_t q1, double* __restrict__ jit) {
+// `base` is converted to jitter while the next block is twisted into the
+// other half; one barrier per block.
+__global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __restrict__ ckpt, FillArgs A,
+                                                          double* __restrict__ jit) {
     __shared__ uint32_t buf[2 * N];
     const int tid = threadIdx.x;
-    for (int j = tid; j < N; j += blockDim.x) buf[j] = ckpt[(size_t)(c0 + blockIdx.x) * N + j];
+    const int64_t c = A.c0 + blockIdx.x;
+    const int np = ckpt_parts(c, A.parts);
+    for (int k = tid; k < N; k += blockDim.x) {
+        uint32_t v = 0;
+        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)c * rtamd::kMTParts + p) * N + k];
+        buf[k] = v;
+    }
     __syncthreads();
-    const int64_t seg_q = (c0 + blockIdx.x) * (int64_t)K * N;
+    const int64_t seg_q = c * (int64_t)A.K * N;
     int base = 0;
-    for (int b = 0; b < K; ++b) {
+    for (int b = 0; b < A.K; ++b) {
         const int64_t bq = seg_q + (int64_t)b * N;   // output index of the block at `base`
-        if (bq >= q1) break;                          // uniform
-        const bool more = b + 1 < K && bq + N < q1;   // uniform
-        const int nb = base ^ N;                      // ring slot of the next block (0 <-> 624)
-        auto R = [&](int k) { return buf[(base + k) % (2 * N)]; };
-        // phase 1 of the next block + conversion of this block
-        if (more)
-            for (int j = tid; j < 227; j += blockDim.x) buf[nb + j] = twist_word(R(j), R(j + 1), R(j + 397));
-        if (bq + N > q0) {
+        if (bq >= A.q1) break;                        // uniform
+        const bool more = b + 1 < A.K && bq + N < A.q1;
+        const int nb = base ^ N;   // (0 <-> 624)
+        if (more) twist_block(buf + base, buf + nb, N);
+        if (bq + N > A.q0) {
             for (int i = tid; i < N / 2; i += blockDim.x) {
                 const int64_t q = bq + 2 * i;
-                if (q >= q0 && q < q1) jit[(q - q0) >> 1] = jitter_from(temper(R(2 * i)), temper(R(2 * i + 1)));
+                if (q >= A.q0 && q < A.q1)
+                    jit[(q - A.q0) >> 1] = jitter_from(temper(buf[base + 2 * i]), temper(buf[base + 2 * i + 1]));
             }
         }
         __syncthreads();
-        if (more) {
-            for (int j = 227 + tid; j < 454; j += blockDim.x) buf[nb + j] = twist_word(R(j), R(j + 1), R(j + 397));
-            __syncthreads();
-            for (int j = 454 + tid; j < N; j += blockDim.x) buf[nb + j] = twist_word(R(j), R(j + 1), R(j + 397));
-            __syncthreads();
-        }
         base = nb;
     }
+}
+
+int level_parts(int64_t n_level) {
+    const int64_t want = (512 + n_level - 1) / n_level;
+    return (int)std::min<int64_t>(rtamd::kMTParts, std::max<int64_t>(1, want));
 }
 
 }  // namespace
 
 namespace rtamd {
 
-hipError_t mt_launch_jitter(const uint32_t* d_base_win, const uint32_t* d_taps, const int32_t* tap_off, int levels,
-                            int K, int64_t q0, int64_t q1, uint32_t* d_ckpt, double* d_jit, hipStream_t stream) {
+hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
+    release();
+    std::vector<uint32_t> polys = mt_tree_polys(K_blocks, levels_needed);
+    std::vector<uint16_t> taps;
+    off.assign(1, 0);
+    for (int j = 0; j < levels_needed; ++j)
+        for (int m = 0; m < kMTRadix; ++m) {
+            if (m > 0) {
+                const uint32_t* P = polys.data() + ((size_t)j * (kMTRadix - 1) + (m - 1)) * kPolyWords32;
+                for (int i = 0; i < kMTDeg; ++i)
+                    if ((P[i >> 5] >> (i & 31)) & 1u) taps.push_back((uint16_t)i);
+            }
+            off.push_back((int32_t)taps.size());
+        }
+    taps.resize(taps.size() + 8, 0);
+    uint32_t win[kMTN];
+    mt_first_window(12345u, win);
+    hipError_t e = hipMalloc(&d_taps, taps.size() * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMalloc(&d_base, sizeof(win));
+    if (e == hipSuccess) e = hipMemcpy(d_taps, taps.data(), taps.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_base, win, sizeof(win), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        release();
+        return e;
+    }
+    K = K_blocks;
+    levels = levels_needed;
+    return hipSuccess;
+}
+
+void JitterPlan::release() {
+    if (d_taps) (void)hipFree(d_taps);
+    if (d_base) (void)hipFree(d_base);
+    d_taps = nullptr;
+    d_base = nullptr;
+    K = levels = 0;
+    off.clear();
+}
+
+hipError_t mt_launch_jitter(const JitterPlan& plan, int64_t q0, int64_t q1, uint32_t* d_ckpt, double* d_jit,
+                            hipStream_t stream) {
     if (q1 <= q0) return hipSuccess;
+    const int K = plan.K;
     const int64_t seg = (int64_t)K * N;
     const int64_t c0 = q0 / seg, c1 = (q1 - 1) / seg;
-    hipError_t e = hipMemcpyAsync(d_ckpt, d_base_win, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
+    if (plan.levels < mt_levels_needed(K, q1) || plan.levels > MAX_LEVELS) return hipErrorInvalidValue;
+    hipError_t e = hipMemcpyAsync(d_ckpt, plan.d_base, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) return e;
-    for (int j = 0; j < levels; ++j) {
-        const int64_t lo = (int64_t)1 << j;
+    int8_t parts[MAX_LEVELS] = {1, 1, 1, 1, 1, 1, 1, 1};
+    for (int j = 0; j < plan.levels; ++j) {
+        const int64_t lo = (int64_t)1 << (3 * j);
+        const int64_t n_j = std::min<int64_t>(lo * 8, c1 + 1) - lo;
+        if (n_j <= 0) break;
+        parts[j] = (int8_t)level_parts(n_j);
+    }
+    for (int j = 0; j < plan.levels; ++j) {
+        const int64_t lo = (int64_t)1 << (3 * j);
         if (lo > c1) break;
-        const int64_t hi = std::min<int64_t>((int64_t)2 << j, c1 + 1);
-        hipLaunchKernelGGL(k_mt_jump_level, dim3((unsigned)(hi - lo)), dim3(JUMP_THREADS), 0, stream,
-                           d_taps + tap_off[j], tap_off[j + 1] - tap_off[j], lo, lo, d_ckpt);
+        const int64_t hi = std::min<int64_t>(lo * 8, c1 + 1);
+        JumpArgs A;
+        A.lo = lo;
+        A.S = parts[j];
+        for (int m = 0; m < 8; ++m) {
+            A.off[m] = plan.off[(size_t)j * 8 + m];
+            A.len[m] = plan.off[(size_t)j * 8 + m + 1] - A.off[m];
+        }
+        for (int k = 0; k < MAX_LEVELS; ++k) A.parts[k] = parts[k];
+        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(hi - lo), (unsigned)A.S), dim3(JUMP_THREADS), 0, stream,
+                           plan.d_taps, A, d_ckpt);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_mt_fill, dim3((unsigned)(c1 - c0 + 1)), dim3(FILL_THREADS), 0, stream, d_ckpt, K, c0, q0,
-                       q1, d_jit);
+    FillArgs F;
+    F.K = K;
+    F.c0 = c0;
+    F.q0 = q0;
+    F.q1 = q1;
+    for (int k = 0; k < MAX_LEVELS; ++k) F.parts[k] = parts[k];
+    hipLaunchKernelGGL(k_mt_fill, dim3((unsigned)(c1 - c0 + 1)), dim3(FILL_THREADS), 0, stream, d_ckpt, F, d_jit);
     return hipGetLastError();
 }
 
-int64_t mt_num_checkpoints(int K, int64_t q1) {
-    if (q1 <= 0) return 1;
-    return (q1 - 1) / ((int64_t)K * N) + 1;
+size_t mt_ckpt_words(int K, int64_t q1) {
+    const int64_t n = q1 > 0 ? (q1 - 1) / ((int64_t)K * N) + 1 : 1;
+    return (size_t)n * kMTParts * N;
 }
 
 int mt_levels_needed(int K, int64_t q1) {
     const int64_t seg = (int64_t)K * N;
-    int64_t cmax = q1 > 0 ? (q1 - 1) / seg : 0;
-    int L = 0;
-    while ((cmax >> L) > 0) ++L;
-    return L < 1 ? 1 : L;
+    const int64_t cmax = q1 > 0 ? (q1 - 1) / seg : 0;   // highest checkpoint index
+    int L = 1;
+    while (((int64_t)1 << (3 * L)) <= cmax) ++L;
+    return L;
 }
 
 }  // namespace rtamd

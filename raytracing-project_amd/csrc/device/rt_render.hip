@@ -361,10 +361,9 @@ struct DBuf {
 struct Workspace {
     std::mutex mu;
     DBuf nodes, mats, lights, objs, ops, gb;
-    DBuf rows, jit, ckpt, polys, basewin, counters;
+    DBuf rows, jit, ckpt, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
-    int polys_levels = 0;
-    std::vector<int32_t> tap_off;
+    rtamd::JitterPlan jplan;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -478,32 +477,20 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
             }
             const int64_t q0 = (int64_t)32 * W * y0, q1 = (int64_t)32 * W * (y1 + 1);
             const int levels = rtamd::mt_levels_needed(kJitterK, q1);
-            if (ws.polys_levels < levels) {
-                std::vector<uint32_t> tab = rtamd::mt_jump_table(kJitterK, levels);
-                std::vector<uint32_t> taps;
-                ws.tap_off.assign(1, 0);
-                for (int j = 0; j < levels; ++j) {
-                    const uint32_t* P = tab.data() + (size_t)j * 624;
-                    for (int i = 0; i < rtamd::kMTDeg; ++i)
-                        if ((P[i >> 5] >> (i & 31)) & 1u) taps.push_back((uint32_t)i);
-                    ws.tap_off.push_back((int32_t)taps.size());
-                }
-                HIP_TRY(upload(ws.polys, taps, st));
-                uint32_t win[624];
-                rtamd::mt_first_window(12345u, win);
-                std::vector<uint32_t> w(win, win + 624);
-                HIP_TRY(upload(ws.basewin, w, st));
+            if (ws.jplan.levels < levels) {
                 HIP_TRY(hipStreamSynchronize(st));
-                ws.polys_levels = levels;
+                try {
+                    HIP_TRY(ws.jplan.build(kJitterK, levels));
+                } catch (const std::exception& ex) {
+                    rtamd::set_last_error(std::string("jitter plan: ") + ex.what());
+                    return RT_ERR_PROCESSING;
+                }
             }
-            const int64_t nck = rtamd::mt_num_checkpoints(kJitterK, q1);
-            HIP_TRY(ws.ckpt.ensure((size_t)nck * 624 * sizeof(uint32_t)));
+            HIP_TRY(ws.ckpt.ensure(rtamd::mt_ckpt_words(kJitterK, q1) * sizeof(uint32_t)));
             HIP_TRY(ws.jit.ensure((size_t)(q1 - q0) / 2 * sizeof(double)));
             HIP_TRY(upload(ws.rows, rows, st));
             HIP_TRY(hipEventRecord(ws.ev[0], st));
-            HIP_TRY(rtamd::mt_launch_jitter(ws.basewin.as<uint32_t>(), ws.polys.as<uint32_t>(), ws.tap_off.data(),
-                                            ws.polys_levels, kJitterK, q0, q1, ws.ckpt.as<uint32_t>(),
-                                            ws.jit.as<double>(), st));
+            HIP_TRY(rtamd::mt_launch_jitter(ws.jplan, q0, q1, ws.ckpt.as<uint32_t>(), ws.jit.as<double>(), st));
             HIP_TRY(hipEventRecord(ws.ev[1], st));
             StdParams P;
             P.W = W;
@@ -678,20 +665,26 @@ extern "C" int rt_framebuffer_to_rgb8_device(const double* fb_dev, size_t n_pixe
 #include "rt_test.h"
 
 extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
+    // Every radix-8 tree polynomial x^(624*K*m*8^j) applied to the seed
+    // window must equal advancing it m*8^j*K twist blocks sequentially.
     try {
-        std::vector<uint32_t> tab = rtamd::mt_jump_table(K_blocks, levels);
+        std::vector<uint32_t> polys = rtamd::mt_tree_polys(K_blocks, levels);
         uint32_t base[624];
         rtamd::mt_first_window(12345u, base);
         int bad = 0;
         for (int j = 0; j < levels; ++j) {
-            uint32_t jumped[624], seq[624];
-            rtamd::mt_apply_jump_cpu(tab.data() + (size_t)j * 624, base, jumped);
+            uint32_t seq[624];
             std::memcpy(seq, base, sizeof(seq));
-            rtamd::mt_advance_blocks_cpu(seq, (uint64_t)K_blocks << j);
-            // bit 31..0 of words 1..623 and the top bit of word 0 define the state
-            bool ok = (jumped[0] & 0x80000000u) == (seq[0] & 0x80000000u);
-            for (int k = 1; k < 624; ++k) ok = ok && jumped[k] == seq[k];
-            if (!ok) ++bad;
+            const uint64_t step = (uint64_t)K_blocks << (3 * j);
+            for (int m = 1; m < rtamd::kMTRadix; ++m) {
+                rtamd::mt_advance_blocks_cpu(seq, step);
+                uint32_t jumped[624];
+                rtamd::mt_apply_jump_cpu(polys.data() + ((size_t)j * 7 + (m - 1)) * 624, base, jumped);
+                // bit 31..0 of words 1..623 and the top bit of word 0 define the state
+                bool ok = (jumped[0] & 0x80000000u) == (seq[0] & 0x80000000u);
+                for (int k = 1; k < 624; ++k) ok = ok && jumped[k] == seq[k];
+                if (!ok) ++bad;
+            }
         }
         return bad;
     } catch (...) {
@@ -704,32 +697,16 @@ extern "C" int rt_test_jitter_device(int64_t q0, int64_t q1, int64_t first, int6
         return RT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
-    const int levels = rtamd::mt_levels_needed(kJitterK, q1);
-    std::vector<uint32_t> tab = rtamd::mt_jump_table(kJitterK, levels);
-    std::vector<uint32_t> taps;
-    std::vector<int32_t> off(1, 0);
-    for (int j = 0; j < levels; ++j) {
-        const uint32_t* P = tab.data() + (size_t)j * 624;
-        for (int i = 0; i < rtamd::kMTDeg; ++i)
-            if ((P[i >> 5] >> (i & 31)) & 1u) taps.push_back((uint32_t)i);
-        off.push_back((int32_t)taps.size());
-    }
-    uint32_t win[624];
-    rtamd::mt_first_window(12345u, win);
-    DBuf dt, dw, dc, dj;
-    HIP_TRY(dt.ensure(taps.size() * 4));
-    HIP_TRY(dw.ensure(624 * 4));
-    HIP_TRY(dc.ensure((size_t)rtamd::mt_num_checkpoints(kJitterK, q1) * 624 * 4));
+    rtamd::JitterPlan plan;
+    HIP_TRY(plan.build(kJitterK, rtamd::mt_levels_needed(kJitterK, q1)));
+    DBuf dc, dj;
+    HIP_TRY(dc.ensure(rtamd::mt_ckpt_words(kJitterK, q1) * 4));
     HIP_TRY(dj.ensure((size_t)(q1 - q0) / 2 * sizeof(double)));
-    HIP_TRY(hipMemcpy(dt.p, taps.data(), taps.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dw.p, win, 624 * 4, hipMemcpyHostToDevice));
-    HIP_TRY(rtamd::mt_launch_jitter(dw.as<uint32_t>(), dt.as<uint32_t>(), off.data(), levels, kJitterK, q0, q1,
-                                    dc.as<uint32_t>(), dj.as<double>(), nullptr));
+    HIP_TRY(rtamd::mt_launch_jitter(plan, q0, q1, dc.as<uint32_t>(), dj.as<double>(), nullptr));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out_host, dj.as<double>() + (first - q0 / 2), (size_t)count * sizeof(double),
                       hipMemcpyDeviceToHost));
-    (void)hipFree(dt.p);
-    (void)hipFree(dw.p);
+    plan.release();
     (void)hipFree(dc.p);
     (void)hipFree(dj.p);
     return RT_OK;

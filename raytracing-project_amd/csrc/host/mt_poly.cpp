@@ -237,6 +237,66 @@ std::vector<uint32_t> mt_jump_table(int K_blocks, int levels) {
     return table;
 }
 
+namespace {
+
+// a * b mod phi (both of degree < 19937), schoolbook carry-less product.
+std::vector<uint64_t> mul_mod(const std::vector<uint64_t>& a, const std::vector<uint64_t>& b, const Reducer& R) {
+    std::vector<uint64_t> q(kW64, 0);
+    const size_t nb = b.size();
+    for (size_t i = 0; i < (size_t)kMTDeg; ++i) {
+        if (!((a[i >> 6] >> (i & 63)) & 1u)) continue;
+        const size_t ws = i >> 6, bs = i & 63;
+        for (size_t w = 0; w < nb && ws + w < q.size(); ++w) {
+            q[ws + w] ^= b[w] << bs;
+            if (bs && ws + w + 1 < q.size()) q[ws + w + 1] ^= b[w] >> (64 - bs);
+        }
+    }
+    R.reduce(q);
+    q.resize(a.size());
+    return q;
+}
+
+std::vector<uint64_t> from_words32(const uint32_t* w, size_t n64) {
+    std::vector<uint64_t> p(n64, 0);
+    for (int j = 0; j < kPolyWords32; ++j)
+        if ((size_t)(j / 2) < n64) p[j / 2] |= (uint64_t)w[j] << ((j & 1) * 32);
+    return p;
+}
+
+}  // namespace
+
+std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels) {
+    static std::map<std::pair<int, int>, std::vector<uint32_t>> cache;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = cache.find({K_blocks, levels});
+        if (it != cache.end()) return it->second;
+    }
+    const auto& phi = mt_charpoly();
+    static Reducer* R = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!R) R = new Reducer(phi);
+    }
+    // base = x^(624*K*8^j), level by level (8^j -> 8^(j+1): three squarings)
+    std::vector<uint32_t> b0 = mt_jump_table(K_blocks, 1);
+    std::vector<uint64_t> base = from_words32(b0.data(), phi.size());
+    std::vector<uint32_t> out;
+    out.reserve((size_t)levels * (kMTRadix - 1) * kPolyWords32);
+    for (int j = 0; j < levels; ++j) {
+        std::vector<uint64_t> pm = base;
+        for (int m = 1; m < kMTRadix; ++m) {
+            if (m > 1) pm = mul_mod(pm, base, *R);
+            std::vector<uint32_t> w = to_words32(pm);
+            out.insert(out.end(), w.begin(), w.end());
+        }
+        for (int k = 1; k < kMTRadix; k <<= 1) square_mod(base, *R);
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    cache[{K_blocks, levels}] = out;
+    return out;
+}
+
 void mt_apply_jump_cpu(const uint32_t* poly, const uint32_t win[kMTN], uint32_t out[kMTN]) {
     std::vector<uint32_t> raw;
     gen_raw(win, (size_t)kMTDeg + kMTN + 1, raw);
