@@ -74,6 +74,15 @@ __device__ __forceinline__ void twist_block(const uint32_t* o, uint32_t* nw, int
     }
 }
 
+// Workgroup barrier ordering LDS only.  __syncthreads() also orders global
+// memory, i.e. waits for the jitter stores of the iteration to complete,
+// which put an HBM write round trip into every twist block of k_mt_fill.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ int ckpt_parts(int64_t c, const int8_t* parts) {
     if (c == 0) return 1;
     const int j = (63 - __builtin_clzll((unsigned long long)c)) / 3;   // c in [8^j, 8^(j+1))
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint16_t* __rest
     __syncthreads();
     for (int b = N; b < JUMP_BUF; b += N) {
         twist_block(buf + b - N, buf + b, JUMP_BUF - b);
-        __syncthreads();
+        lds_barrier();
     }
     if (tid < N / 2) {
         uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __rest
                     jit[(q - A.q0) >> 1] = jitter_from(temper(buf[base + 2 * i]), temper(buf[base + 2 * i + 1]));
             }
         }
-        __syncthreads();
+        lds_barrier();
         base = nb;
     }
 }
