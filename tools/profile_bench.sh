@@ -16,4 +16,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_$i -o pmc -- python bench.py --steps 1 --warmup 1 --no-cpu > $OUT/pmc_$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
-python tools/summarize_profile.py $OUT profiles $TAG
+python tools/summarize_profile.py $OUT $OUT/summary $TAG  # copy into profiles/ locally after the call
