@@ -57,6 +57,7 @@ def main() -> int:
     ap.add_argument("--cpu-rows", type=int, default=64, help="rows in the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cull", action="store_true", help="disable wave-uniform bound culling")
+    ap.add_argument("--chunks", type=int, default=4, help="row chunks per rank pipelined with the gather (N > 1)")
     args = ap.parse_args()
 
     import numpy as np
@@ -75,7 +76,7 @@ def main() -> int:
     import frame_dist
     import rtamd
     import scenes
-    from frame_dist import STRIP, strip_rows
+    from frame_dist import STRIP
 
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
@@ -84,39 +85,42 @@ def main() -> int:
     flags = rtamd.RT_FLAG_NO_CULL if args.no_cull else rtamd.RT_FLAG_NONE
     dev = torch.device("cuda", local)
 
-    rows = strip_rows(H, rank, world)
+    df = frame_dist.DistFrame(W, H, rank, world, dev, chunks=args.chunks)
+    rows = df.rows
     n_rows = len(rows)
     rows_c = (C.c_int32 * max(1, n_rows))(*rows)
-    max_rows = frame_dist.max_rows(H, world)
-    fb_rows = torch.zeros((max_rows, W, 3), dtype=torch.float64, device=dev)
-    full = torch.zeros((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
-    gathered = None
-    all_rows_dev = None
-    if world > 1:
-        gathered = torch.zeros((world * max_rows, W, 3), dtype=torch.float64, device=dev) if True else None
-        if rank == 0:
-            all_rows_dev = torch.tensor(frame_dist.gather_row_index(H, world), dtype=torch.int32, device=dev)
-
     stream = torch.cuda.current_stream(dev)
     st = rtamd.Stats()
 
-    def step(f=flags, stats=st):
-        rc = lib.rt_render_rows_device(sc.handle, W, H, mode, f, rows_c, n_rows, C.c_void_p(fb_rows.data_ptr()),
-                                       C.c_void_p(stream.cuda_stream), C.byref(stats))
+    def scatter(stage, slot_rows, full):
+        rc = lib.rt_scatter_rows_device(C.c_void_p(stage.data_ptr()), C.c_void_p(slot_rows.data_ptr()),
+                                        slot_rows.numel(), W, C.c_void_p(full.data_ptr()),
+                                        C.c_void_p(stream.cuda_stream))
         if rc != 0:
-            raise RuntimeError(f"rt_render_rows_device failed ({rc}): {rtamd.last_error()}")
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, fb_rows)
-            if rank == 0:
-                # padded slots carry row -1: scatter only the real rows
-                for r in range(world):
-                    nr = len(strip_rows(H, r, world))
-                    lib.rt_scatter_rows_device(C.c_void_p(gathered[r * max_rows].data_ptr()),
-                                               C.c_void_p(all_rows_dev[r * max_rows:].data_ptr()), nr, W,
-                                               C.c_void_p(full.data_ptr()), C.c_void_p(stream.cuda_stream))
-        elif rank == 0:
-            lib.rt_scatter_rows_device(C.c_void_p(fb_rows.data_ptr()), C.c_void_p(0), 0, W,
-                                       C.c_void_p(full.data_ptr()), C.c_void_p(stream.cuda_stream))
+            raise RuntimeError(f"rt_scatter_rows_device failed ({rc}): {rtamd.last_error()}")
+
+    def step(f=flags, stats=st):
+        # one frame: jitter stream of this rank's rows (rt_frame_begin), the
+        # trace chunk by chunk, each chunk gathered to rank 0 over RCCL while
+        # the next one is traced (frame_dist.DistFrame), scatter on rank 0
+        fr = C.c_void_p()
+        rc = lib.rt_frame_begin(sc.handle, W, H, mode, f, rows_c, n_rows, C.c_void_p(stream.cuda_stream),
+                                C.byref(fr))
+        if rc != 0:
+            raise RuntimeError(f"rt_frame_begin failed ({rc}): {rtamd.last_error()}")
+        err = []
+
+        def trace_chunk(a, b, out):
+            r = lib.rt_frame_trace(fr, a, b, C.c_void_p(out.data_ptr()))
+            if r != 0:
+                err.append((r, rtamd.last_error()))
+
+        try:
+            df.run(trace_chunk, dist, scatter)
+        finally:
+            rc = lib.rt_frame_end(fr, C.byref(stats))
+        if err or rc != 0:
+            raise RuntimeError(f"frame failed: {err or rc} {rtamd.last_error()}")
 
     for _ in range(args.warmup):
         step()
@@ -206,7 +210,7 @@ def main() -> int:
         "dtype": "f64",
         "data": "synthetic: reference example scene JSON + mt19937(12345) jitter, rendered on device",
         "config": {"workload": name, "width": W, "height": H, "mode": "paper" if mode else "standard",
-                   "rays_per_frame": int(rays_per_frame), "parallelism": f"row-strips{STRIP}x{world}",
+                   "rays_per_frame": int(rays_per_frame), "parallelism": f"row-strips{STRIP}x{world}" + (f", gather-to-rank0 in {len(df.bounds)} chunks" if world > 1 else ""),
                    "cull": not args.no_cull},
         "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),

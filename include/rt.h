@@ -14,6 +14,8 @@
  *                               raytracer/src/tracer.cpp:247-305, tracer.h:18-35
  *   rt_render_rows_device    <- the same loop restricted to a set of output
  *                               rows (multi-GPU row tiling)
+ *   rt_frame_begin/trace/end <- the same loop, split so that row chunks can
+ *                               be gathered while later chunks are traced
  *   rt_scatter_rows_device   <- (no reference equivalent: places gathered row
  *                               bands into the full framebuffer on rank 0)
  *   rt_framebuffer_to_rgb8   <- framebuffer_to_mat_bgr8 / toByte
@@ -205,12 +207,32 @@ int rt_render(const rt_scene* s, int W, int H, int mode, int flags,
 
 /* Render an arbitrary set of OUTPUT rows (top-row-first indices) into a
  * compact device buffer fb_rows_dev[n_rows][W][3] on the given HIP stream
- * (NULL = default stream).  rows_host lists the rows.  Blocks until done. */
+ * (NULL = default stream).  rows_host lists the rows, distinct, in any order
+ * (a duplicate is RT_ERR_INVALID_ARG).  Only the jitter-stream segments those
+ * rows consume are generated.  Blocks until done. */
 int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, int flags,
                           const int32_t* rows_host, int n_rows,
                           double* fb_rows_dev, void* hip_stream, rt_stats* stats);
 
-/* fb_dev[rows[i]][*] = src_dev[i][*] for i < n_rows (device copy, W*3 doubles per row). */
+/* Frame pipeline: rt_render_rows_device split into an asynchronous begin /
+ * trace / end, so that a multi-GPU rank can hand finished row chunks to a
+ * collective (RCCL on its own stream) while the next chunks are traced
+ * (SURVEY.md §8e).  rt_frame_begin validates the rows (as
+ * rt_render_rows_device), uploads the scene and enqueues the jitter stream of
+ * ALL the listed rows; rt_frame_trace enqueues the trace of list entries
+ * [ri0, ri1) into fb_rows_dev[0 .. ri1-ri0) (each list entry traced once);
+ * rt_frame_end waits for the stream, fills stats and frees the frame — call
+ * it exactly once per begun frame, also after an error.  begin/trace only
+ * enqueue work on hip_stream.  One frame per device at a time (begin blocks
+ * while another frame of the same device is open). */
+typedef struct rt_frame rt_frame;
+int rt_frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
+                   void* hip_stream, rt_frame** out);
+int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev);
+int rt_frame_end(rt_frame* f, rt_stats* stats);
+
+/* fb_dev[rows[i]][*] = src_dev[i][*] for i < n_rows (device copy, W*3 doubles per row);
+ * slots with rows[i] < 0 (padding) are skipped. */
 int rt_scatter_rows_device(const double* src_dev, const int32_t* rows_dev, int n_rows,
                            int W, double* fb_dev, void* hip_stream);
 

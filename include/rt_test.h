@@ -19,9 +19,10 @@ extern "C" {
 int rt_test_mt_jump_cpu(int K_blocks, int levels);
 
 /* GPU: generate the jitter stream for output indices [q0, q1) (even) with the
- * device jump/fill kernels and copy uniform draws [first, first+count) (draw
- * index = output index / 2) to out_host.  Returns an rt_status. */
-int rt_test_jitter_device(int64_t q0, int64_t q1, int64_t first, int64_t count, double* out_host);
+ * device jump/fill kernels at segment length K_blocks twist blocks and copy
+ * uniform draws [first, first+count) (draw index = output index / 2) to
+ * out_host.  Returns an rt_status. */
+int rt_test_jitter_device(int K_blocks, int64_t q0, int64_t q1, int64_t first, int64_t count, double* out_host);
 
 /* Host-only: compile a scene to its device object table and report
  * out[8] = {objects incl. cull headers, object cull groups, their members,

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 
 #include "mt_jump.hpp"
 #include "mt_poly.hpp"
@@ -30,31 +31,16 @@ constexpr int N = 624;
 constexpr int DEG = 19937;
 constexpr int JUMP_BUF = DEG + N;   // raw words w_n .. w_{n+DEG+N-1}
 constexpr int JUMP_THREADS = 320;   // 312 correlation lanes x 2 outputs
-constexpr int FILL_THREADS = 256;
-constexpr int MAX_LEVELS = 8;
+// k_mt_fill roles: waves 0-3 twist the next block (227 lanes), waves 4-8
+// convert the current one (312 output pairs, one per lane), so the two
+// latency chains of a block overlap instead of running back to back.
+constexpr int FILL_TWIST = 256;
+constexpr int FILL_THREADS = FILL_TWIST + 320;
+constexpr int MAX_LEVELS = rtamd::kMTMaxLevels;
 
 __device__ __forceinline__ uint32_t twist_word(uint32_t wk, uint32_t wk1, uint32_t wk397) {
     const uint32_t y = (wk & 0x80000000u) | (wk1 & 0x7fffffffu);
     return wk397 ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-}
-
-__device__ __forceinline__ uint32_t temper(uint32_t y) {
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
-}
-
-// generate_canonical<double,53> over two outputs, then
-// uniform_real_distribution(-0.5,0.5): (u * (b - a)) + a (random.h:1870).
-__device__ __forceinline__ double jitter_from(uint32_t w0, uint32_t w1) {
-    double sum = 0.0;
-    sum += (double)w0 * 1.0;
-    sum += (double)w1 * 4294967296.0;
-    double ret = sum / 18446744073709551616.0;
-    if (ret >= 1.0) ret = 0x1.fffffffffffffp-1;   // nextafter(1, 0)
-    return (ret * (0.5 - -0.5)) + -0.5;
 }
 
 // One twist block: nw[0..N) from the previous block o[0..N) (disjoint LDS
@@ -90,7 +76,8 @@ __device__ __forceinline__ int ckpt_parts(int64_t c, const int8_t* parts) {
 }
 
 struct JumpArgs {
-    int64_t lo;                 // 8^j: this level computes c in [lo, lo + gridDim.x)
+    int64_t lo;                 // 8^j: this level computes checkpoints in [lo, 8*lo)
+    const int64_t* list;        // the checkpoints of this level to compute (gridDim.x of them)
     int S;                      // partial jumps per checkpoint (gridDim.y)
     int32_t off[8], len[8];     // tap slice of x^(624*K*m*8^j), m = c / lo
     int8_t parts[MAX_LEVELS];   // partial count of the checkpoints of every level
@@ -106,7 +93,7 @@ __global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint16_t* __rest
                                                           uint32_t* __restrict__ ckpt) {
     __shared__ uint32_t buf[JUMP_BUF + 8];
     __shared__ __attribute__((aligned(16))) uint16_t tp[MAX_TAPS];
-    const int64_t c = A.lo + blockIdx.x;
+    const int64_t c = A.list[blockIdx.x];
     const int s = blockIdx.y;
     const int m = (int)(c / A.lo);
     const int64_t r = c - (int64_t)m * A.lo;
@@ -157,49 +144,115 @@ __global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint16_t* __rest
 
 struct FillArgs {
     int K;
-    int64_t c0, q0, q1;
+    int nr;                      // number of ranges
+    const rtamd::JRange* R;      // sorted, disjoint output ranges
+    const int64_t* segs;         // per workgroup: (segment c, first range overlapping it)
     int8_t parts[MAX_LEVELS];
 };
 
-// One workgroup per segment: regenerate K blocks from the checkpoint and
-// write jitter for outputs in [q0, q1).  buf is a 2-block ring: the block at
-// `base` is converted to jitter while the next block is twisted into the
-// other half; one barrier per block.
+// Where the draws of one block go: output pair i (outputs bq+2i, bq+2i+1)
+// is stored at p0[i] for i in [a0, b0) and at p1[i] for i in [a1, b1)
+// (block-uniform); rows narrower than 20 pixels put more than two ranges
+// into a block and take the generic path.
+struct BlockDst {
+    double* p0;
+    double* p1;
+    int a0, b0, a1, b1;
+    bool generic;
+};
+
+__device__ __forceinline__ int clampP(int64_t v) { return v < 0 ? 0 : v > N / 2 ? N / 2 : (int)v; }
+
+__device__ __forceinline__ BlockDst block_dst(double* jit, int64_t bq, const rtamd::JRange& g0,
+                                              const rtamd::JRange& g1, int r, int nr) {
+    BlockDst d;
+    d.a0 = clampP((g0.qa - bq) >> 1);
+    d.b0 = clampP((g0.qb - bq) >> 1);
+    d.a1 = clampP((g1.qa - bq) >> 1);
+    d.b1 = clampP((g1.qb - bq) >> 1);
+    d.p0 = jit + (g0.dst - ((g0.qa - bq) >> 1));
+    d.p1 = jit + (g1.dst - ((g1.qa - bq) >> 1));
+    d.generic = g1.qb - bq < N && r + 2 < nr;
+    return d;
+}
+
+__device__ __forceinline__ int64_t generic_dst(int64_t q, const FillArgs& A, int r) {
+    for (int k = r; k < A.nr && q >= A.R[k].qa; ++k)
+        if (q < A.R[k].qb) return A.R[k].dst + ((q - A.R[k].qa) >> 1);
+    return -1;
+}
+
+// generate_canonical<double,53> over two tempered outputs, then
+// uniform_real_distribution(-0.5,0.5) (mt_jump.hpp jitter_draw).
+__device__ __forceinline__ double jitter_from(uint32_t raw0, uint32_t raw1) { return rtamd::jitter_draw(raw0, raw1); }
+
+// One workgroup per needed segment: regenerate its blocks from the
+// checkpoint and write the jitter of every output that falls in a range.
+// Blocks live in a 2-block LDS ring with one barrier per block: while the
+// twist waves compute block b+1 from block b, the convert waves turn block b
+// into draws and store them.  The range cursor r is workgroup-uniform (scalar registers).
 __global__ __launch_bounds__(FILL_THREADS) void k_mt_fill(const uint32_t* __restrict__ ckpt, FillArgs A,
                                                           double* __restrict__ jit) {
     __shared__ uint32_t buf[2 * N];
     const int tid = threadIdx.x;
-    const int64_t c = A.c0 + blockIdx.x;
+    const int64_t c = A.segs[2 * blockIdx.x];
+    int r = (int)A.segs[2 * blockIdx.x + 1];
     const int np = ckpt_parts(c, A.parts);
-    for (int k = tid; k < N; k += blockDim.x) {
+    const int64_t seg_q = c * (int64_t)A.K * N;
+    const int64_t q_last = A.R[A.nr - 1].qb;
+    // ranges r and r+1 cached in scalar registers
+    rtamd::JRange g0 = A.R[r];
+    rtamd::JRange g1 = r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
+    for (int k = tid; k < N; k += blockDim.x) {   // block 0 = the checkpoint window
         uint32_t v = 0;
         for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)c * rtamd::kMTParts + p) * N + k];
         buf[k] = v;
     }
     __syncthreads();
-    const int64_t seg_q = c * (int64_t)A.K * N;
-    int base = 0;
+    int base = 0;   // ring slot of block b
     for (int b = 0; b < A.K; ++b) {
-        const int64_t bq = seg_q + (int64_t)b * N;   // output index of the block at `base`
-        if (bq >= A.q1) break;                        // uniform
-        const bool more = b + 1 < A.K && bq + N < A.q1;
-        const int nb = base ^ N;   // (0 <-> 624)
-        if (more) twist_block(buf + base, buf + nb, N);
-        if (bq + N > A.q0) {
-            for (int i = tid; i < N / 2; i += blockDim.x) {
-                const int64_t q = bq + 2 * i;
-                if (q >= A.q0 && q < A.q1)
-                    jit[(q - A.q0) >> 1] = jitter_from(temper(buf[base + 2 * i]), temper(buf[base + 2 * i + 1]));
+        const int64_t bq = seg_q + (int64_t)b * N;   // first output fed by block b
+        if (bq >= q_last) break;
+        while (g0.qb <= bq) {                         // uniform
+            if (++r >= A.nr) break;
+            g0 = g1;
+            g1 = r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
+        }
+        if (r >= A.nr) break;
+        const uint32_t* o = buf + base;
+        if (tid < FILL_TWIST) {
+            if (b + 1 < A.K && bq + N < q_last) twist_block(o, buf + (base ^ N), N);
+        } else if (g0.qa < bq + N) {
+            const int i = tid - FILL_TWIST;   // output pair i of the block
+            if (i < N / 2) {
+                const BlockDst d = block_dst(jit, bq, g0, g1, r, A.nr);
+                double* dst = nullptr;
+                if (d.generic) {
+                    const int64_t q = generic_dst(bq + 2 * i, A, r);
+                    if (q >= 0) dst = jit + q;
+                } else if (i >= d.a0 && i < d.b0) {
+                    dst = d.p0 + i;
+                } else if (i >= d.a1 && i < d.b1) {
+                    dst = d.p1 + i;
+                }
+                if (dst) *dst = jitter_from(o[2 * i], o[2 * i + 1]);
             }
         }
         lds_barrier();
-        base = nb;
+        base ^= N;
     }
 }
 
 int level_parts(int64_t n_level) {
     const int64_t want = (512 + n_level - 1) / n_level;
     return (int)std::min<int64_t>(rtamd::kMTParts, std::max<int64_t>(1, want));
+}
+
+// Level of checkpoint c >= 1 in the radix-8 tree and its parent.
+inline int ckpt_level(int64_t c) { return (63 - __builtin_clzll((unsigned long long)c)) / 3; }
+inline int64_t ckpt_parent(int64_t c) {
+    const int64_t lo = (int64_t)1 << (3 * ckpt_level(c));
+    return c - (c / lo) * lo;
 }
 
 }  // namespace
@@ -245,46 +298,99 @@ void JitterPlan::release() {
     off.clear();
 }
 
-hipError_t mt_launch_jitter(const JitterPlan& plan, int64_t q0, int64_t q1, uint32_t* d_ckpt, double* d_jit,
-                            hipStream_t stream) {
-    if (q1 <= q0) return hipSuccess;
+size_t mt_scratch_bytes(int K, const std::vector<JRange>& ranges) {
+    if (ranges.empty()) return 64;
+    const int64_t n_ck = (ranges.back().qb - 1) / ((int64_t)K * N) + 1;
+    return ranges.size() * sizeof(JRange) + (size_t)n_ck * 3 * sizeof(int64_t) + 64;
+}
+
+hipError_t mt_launch_jitter(const JitterPlan& plan, const std::vector<JRange>& ranges, JitterJob& job,
+                            void* d_scratch, uint32_t* d_ckpt, double* d_jit, hipStream_t stream) {
+    if (ranges.empty()) return hipSuccess;
+    for (size_t i = 0; i < ranges.size(); ++i) {
+        const JRange& g = ranges[i];
+        if (g.qa < 0 || g.qb <= g.qa || (g.qa & 1) || (g.qb & 1) || g.dst < 0 ||
+            (i && g.qa < ranges[i - 1].qb))
+            return hipErrorInvalidValue;
+    }
     const int K = plan.K;
     const int64_t seg = (int64_t)K * N;
-    const int64_t c0 = q0 / seg, c1 = (q1 - 1) / seg;
-    if (plan.levels < mt_levels_needed(K, q1) || plan.levels > MAX_LEVELS) return hipErrorInvalidValue;
-    hipError_t e = hipMemcpyAsync(d_ckpt, plan.d_base, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
+    const int64_t qmax = ranges.back().qb;
+    const int64_t c1 = (qmax - 1) / seg;
+    if (plan.levels < mt_levels_needed(K, qmax) || plan.levels > MAX_LEVELS) return hipErrorInvalidValue;
+
+    // needed segments (with their first overlapping range) and the tree
+    // ancestors of each: checkpoint c is one jump from ckpt_parent(c)
+    std::vector<int64_t> segs;
+    std::vector<char> need((size_t)c1 + 1, 0);
+    {
+        size_t r = 0;
+        int64_t last = -1;
+        for (const JRange& g : ranges) {
+            for (int64_t c = std::max(last + 1, g.qa / seg); c <= (g.qb - 1) / seg; ++c) {
+                while (r < ranges.size() && ranges[r].qb <= c * seg) ++r;
+                segs.push_back(c);
+                segs.push_back((int64_t)r);
+                for (int64_t a = c; a > 0 && !need[a]; a = ckpt_parent(a)) need[a] = 1;
+                last = c;
+            }
+        }
+    }
+    std::vector<int64_t> lists;
+    int64_t lvl_off[MAX_LEVELS + 1] = {0};
+    for (int j = 0; j < plan.levels; ++j) {
+        const int64_t lo = (int64_t)1 << (3 * j);
+        for (int64_t c = lo; c <= std::min(c1, lo * 8 - 1); ++c)
+            if (need[c]) lists.push_back(c);
+        lvl_off[j + 1] = (int64_t)lists.size();
+    }
+    // stage: ranges | segs | per-level lists
+    const size_t b_r = ranges.size() * sizeof(JRange), b_s = segs.size() * sizeof(int64_t),
+                 b_l = lists.size() * sizeof(int64_t);
+    job.stage.resize(b_r + b_s + b_l);
+    std::memcpy(job.stage.data(), ranges.data(), b_r);
+    std::memcpy(job.stage.data() + b_r, segs.data(), b_s);
+    if (b_l) std::memcpy(job.stage.data() + b_r + b_s, lists.data(), b_l);
+    job.qmax = qmax;
+    char* dsc = static_cast<char*>(d_scratch);
+    hipError_t e = hipMemcpyAsync(dsc, job.stage.data(), job.stage.size(), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    const JRange* dR = reinterpret_cast<const JRange*>(dsc);
+    const int64_t* dS = reinterpret_cast<const int64_t*>(dsc + b_r);
+    const int64_t* dL = reinterpret_cast<const int64_t*>(dsc + b_r + b_s);
+
+    e = hipMemcpyAsync(d_ckpt, plan.d_base, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) return e;
     int8_t parts[MAX_LEVELS] = {1, 1, 1, 1, 1, 1, 1, 1};
     for (int j = 0; j < plan.levels; ++j) {
-        const int64_t lo = (int64_t)1 << (3 * j);
-        const int64_t n_j = std::min<int64_t>(lo * 8, c1 + 1) - lo;
-        if (n_j <= 0) break;
-        parts[j] = (int8_t)level_parts(n_j);
+        const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
+        if (n_j > 0) parts[j] = (int8_t)level_parts(n_j);
     }
     for (int j = 0; j < plan.levels; ++j) {
-        const int64_t lo = (int64_t)1 << (3 * j);
-        if (lo > c1) break;
-        const int64_t hi = std::min<int64_t>(lo * 8, c1 + 1);
+        const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
+        if (n_j <= 0) continue;
         JumpArgs A;
-        A.lo = lo;
+        A.lo = (int64_t)1 << (3 * j);
+        A.list = dL + lvl_off[j];
         A.S = parts[j];
         for (int m = 0; m < 8; ++m) {
             A.off[m] = plan.off[(size_t)j * 8 + m];
             A.len[m] = plan.off[(size_t)j * 8 + m + 1] - A.off[m];
         }
         for (int k = 0; k < MAX_LEVELS; ++k) A.parts[k] = parts[k];
-        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)(hi - lo), (unsigned)A.S), dim3(JUMP_THREADS), 0, stream,
+        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_j, (unsigned)A.S), dim3(JUMP_THREADS), 0, stream,
                            plan.d_taps, A, d_ckpt);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     FillArgs F;
     F.K = K;
-    F.c0 = c0;
-    F.q0 = q0;
-    F.q1 = q1;
+    F.nr = (int)ranges.size();
+    F.R = dR;
+    F.segs = dS;
     for (int k = 0; k < MAX_LEVELS; ++k) F.parts[k] = parts[k];
-    hipLaunchKernelGGL(k_mt_fill, dim3((unsigned)(c1 - c0 + 1)), dim3(FILL_THREADS), 0, stream, d_ckpt, F, d_jit);
+    hipLaunchKernelGGL(k_mt_fill, dim3((unsigned)(segs.size() / 2)), dim3(FILL_THREADS), 0, stream, d_ckpt, F,
+                       d_jit);
     return hipGetLastError();
 }
 

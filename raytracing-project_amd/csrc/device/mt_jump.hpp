@@ -12,6 +12,7 @@ namespace rtamd {
 // partial windows whose XOR is the window: a jump is split across several
 // workgroups by tap ranges, each writing its own partial.
 constexpr int kMTParts = 8;
+constexpr int kMTMaxLevels = 8;
 
 // Host-built plan for one segment length K: the radix-8 tree's tap lists
 // (exponents with coefficient 1 in x^(624*K*m*8^j) mod phi, csrc/host/
@@ -26,10 +27,54 @@ struct JitterPlan {
     void release();
 };
 
-// Writes jit[(q - q0)/2] for even q in [q0, q1) (q0, q1 even).  d_ckpt must
-// hold mt_ckpt_words(K, q1) words; plan.levels >= mt_levels_needed(K, q1).
-hipError_t mt_launch_jitter(const JitterPlan& plan, int64_t q0, int64_t q1, uint32_t* d_ckpt, double* d_jit,
-                            hipStream_t stream);
+// A run of stream outputs: the draw made of outputs q, q+1 (q even, in
+// [qa, qb)) is stored at jit[dst + (q - qa)/2].  Ranges passed to the
+// launcher are sorted by qa and disjoint.  A rendered loop row y of width W
+// is the range [32*W*y, 32*W*(y+1)) (tracer.cpp:284-293: 8 samples x 2
+// draws x 2 words).
+struct JRange {
+    int64_t qa, qb, dst;
+};
+
+// mt19937 tempering (libstdc++ random.tcc operator()).
+__host__ __device__ __forceinline__ uint32_t mt_temper_word(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+// One jitter draw from two raw (untempered) words: tempering, generate_canonical<double,
+// 53> over the two outputs (random.tcc:3348-3378), then
+// uniform_real_distribution(-0.5, 0.5): (u * (b - a)) + a (random.h:1870).
+// Callers compile without FP contraction, so every step rounds as on x86-64.
+__host__ __device__ __forceinline__ double jitter_draw(uint32_t raw0, uint32_t raw1) {
+    double sum = 0.0;
+    sum += (double)mt_temper_word(raw0) * 1.0;
+    sum += (double)mt_temper_word(raw1) * 4294967296.0;
+    double ret = sum / 18446744073709551616.0;
+    if (ret >= 1.0) ret = 0x1.fffffffffffffp-1;   // nextafter(1, 0)
+    return (ret * (0.5 - -0.5)) + -0.5;
+}
+
+// Host-side state of one launch: device lists (segments to regenerate,
+// checkpoints per tree level, ranges) are staged here and uploaded into the
+// caller's device scratch; the host copy stays alive until the stream is
+// synchronised.
+struct JitterJob {
+    std::vector<char> stage;
+    int64_t qmax = 0;
+};
+
+// Only the checkpoints the requested ranges need are computed (the needed
+// segments and their tree ancestors) and only the segments that overlap a
+// range are regenerated, so a rank rendering 1/N of the rows does ~1/N of
+// the jump work.  d_scratch must hold mt_scratch_bytes(ranges) bytes, d_ckpt
+// mt_ckpt_words(K, qmax) words; plan.levels >= mt_levels_needed(K, qmax).
+hipError_t mt_launch_jitter(const JitterPlan& plan, const std::vector<JRange>& ranges, JitterJob& job,
+                            void* d_scratch, uint32_t* d_ckpt, double* d_jit, hipStream_t stream);
+size_t mt_scratch_bytes(int K, const std::vector<JRange>& ranges);
 size_t mt_ckpt_words(int K, int64_t q1);
 int mt_levels_needed(int K, int64_t q1);
 

@@ -11,9 +11,12 @@
 //   k_paper_finish: edge strength from the stored neighbour hits + hatch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -31,14 +34,32 @@ namespace {
 
 constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
 constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics
-constexpr int kJitterK = 1024;          // twist blocks per jitter segment
+constexpr int kJitterK = 1024;          // twist blocks per jitter segment (whole frames)
+constexpr int kJitterKSmall = 512;      // ... for row subsets (multi-GPU ranks)
+
+// Segment length for a jitter job: a segment is regenerated serially by one
+// workgroup (latency ~ K twist blocks), a checkpoint costs one GF(2) jump
+// (~10k-tap correlation over 20k words in LDS).  Whole frames amortise the
+// jumps with long segments; a rank that needs a fraction of the stream has
+// fewer checkpoints to jump to, so shorter segments cut its fill latency.
+// RT_JITTER_K overrides (diagnostics).
+int jitter_k(int64_t words_needed, int64_t q_max) {
+    static const int env_k = [] {
+        const char* e = std::getenv("RT_JITTER_K");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (env_k > 0) return env_k;
+    // measured on config 4 (tools/sim_ranks.py): 1024 wins for whole frames,
+    // 512 from half a frame down (8 ranks: 0.62 -> 0.53 ms)
+    return words_needed * 4 > q_max * 3 ? kJitterK : kJitterKSmall;
+}
 
 struct StdParams {
     int W, H;
     int n_rows;
-    int jy0;
     const int32_t* rows;
-    const double* jit;
+    const int32_t* jrow;   // jitter row of every listed row
+    const double* jit;     // 16 draws per pixel: (dx, dy) of samples 0..7
     double* fb;
     unsigned long long* counters;
 };
@@ -98,7 +119,8 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     if (active) {
         const int r = P.rows[ri];
         const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
-        const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)(y - P.jy0) * P.W + x) * 16 + 2 * s);
+        // draws 16p+2s, 16p+2s+1 of the stream: dx, dy (tracer.cpp:293)
+        const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)P.jrow[ri] * P.W + x) * 16 + 2 * s);
         const DRay ray = gen_ray_subpixel(S, x, y, j.x, j.y);
         c = trace<E, D, SEC>(S, ray, ni, no, cnt);
     }
@@ -139,6 +161,8 @@ struct PaperParams {
     int W, H;
     int n_ext;
     int n_rows;
+    int n_list;                  // primary pass: ext indices ext_list[0..n_list) of this launch
+    const int32_t* ext_list;
     const int32_t* ext_rows;     // rows needing a primary hit
     const int32_t* ext_shade;    // 1 = row is rendered by this call (shade it)
     const int32_t* nbr;          // per rendered row: ext index of r-1, r, r+1 (-1 = outside frame)
@@ -160,11 +184,12 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ei = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = x < P.W && ei < P.n_ext;
+    const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < P.W && li < P.n_list;
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
     if (active) {
+        const int ei = P.ext_list[li];
         const int y = P.ext_rows[ei];
         const DRay r = gen_ray(S, x, y);
         double ht = 0.0;
@@ -282,7 +307,8 @@ __global__ void k_scatter_rows(const double* __restrict__ src, const int32_t* __
     const size_t total = row_len * n_rows;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const size_t r = i / row_len, k = i - r * row_len;
-        dst[(size_t)rows[r] * row_len + k] = src[i];
+        const int32_t d = rows[r];
+        if (d >= 0) dst[(size_t)d * row_len + k] = src[i];
     }
 }
 
@@ -361,9 +387,11 @@ struct DBuf {
 struct Workspace {
     std::mutex mu;
     DBuf nodes, mats, lights, objs, ops, gb;
-    DBuf rows, jit, ckpt, counters;
+    DBuf rows, jit, ckpt, jscratch, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
-    rtamd::JitterPlan jplan;
+    rtamd::JitterPlan jplan[2];   // K = kJitterK, kJitterKSmall (or the override)
+    rtamd::JitterJob jjob;
+    std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
@@ -384,15 +412,54 @@ hipError_t upload(DBuf& b, const std::vector<T>& v, hipStream_t st) {
     return hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, st);
 }
 
-int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
-                     double* fb_dev, hipStream_t st, rt_stats* stats) {
+}  // namespace
+
+// One frame in flight on one device (rt_frame_begin .. rt_frame_end).  Holds
+// the device workspace lock for its lifetime; every launch is stream-ordered
+// on `st`, and every host buffer an async upload reads stays alive here
+// until rt_frame_end has synchronised the stream.
+struct rt_frame {
+    Workspace* ws = nullptr;
+    std::unique_lock<std::mutex> lock;
+    hipStream_t st = nullptr;
+    DevScene S;
+    int W = 0, H = 0, mode = 0, n_rows = 0;
+    bool eager = false, deep = false, secondary = false, count_ops = false;
+    bool traced = false;
+    std::vector<int32_t> rows;
+    std::vector<int32_t> rows_jrow;            // standard mode: rows | jitter row of each
+    std::chrono::steady_clock::time_point t_start;
+    uint64_t logical_isect = 0;
+    // paper mode: ext = rendered rows and their vertical neighbours
+    int n_ext = 0;
+    std::vector<int32_t> ext_pos;              // output row -> ext index (-1: none)
+    std::vector<char> ext_done;                // primary hit already launched
+    int list_used = 0;                         // ext-list entries consumed in the aux buffer
+    std::vector<std::vector<int32_t>> stage;   // host sources of async uploads
+    rtamd::CompiledScene cs;
+    std::vector<rt_node> nodes;
+    std::vector<rt_material> mats;
+    std::vector<rt_light> lights;
+};
+
+namespace {
+
+int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
+                hipStream_t st, rt_frame** out) {
     const auto t_start = std::chrono::steady_clock::now();
+    if (!out) { rtamd::set_last_error("rt_frame_begin: out is NULL"); return RT_ERR_INVALID_ARG; }
+    *out = nullptr;
     if (!s) { rtamd::set_last_error("rt_render: scene is NULL"); return RT_ERR_INVALID_ARG; }
     if (W <= 0 || H <= 0) { rtamd::set_last_error("rt_render: W and H must be > 0"); return RT_ERR_INVALID_ARG; }
     if (mode != RT_MODE_STANDARD && mode != RT_MODE_PAPER) { rtamd::set_last_error("rt_render: bad mode"); return RT_ERR_INVALID_ARG; }
-    if (n_rows < 0 || (n_rows > 0 && (!rows_host || !fb_dev))) { rtamd::set_last_error("rt_render: bad rows/fb"); return RT_ERR_INVALID_ARG; }
-    for (int i = 0; i < n_rows; ++i)
-        if (rows_host[i] < 0 || rows_host[i] >= H) { rtamd::set_last_error("rt_render: row out of range"); return RT_ERR_INVALID_ARG; }
+    if (n_rows < 0 || (n_rows > 0 && !rows_host)) { rtamd::set_last_error("rt_render: bad rows"); return RT_ERR_INVALID_ARG; }
+    {
+        std::vector<char> seen(H, 0);
+        for (int i = 0; i < n_rows; ++i) {
+            if (rows_host[i] < 0 || rows_host[i] >= H) { rtamd::set_last_error("rt_render: row out of range"); return RT_ERR_INVALID_ARG; }
+            if (seen[rows_host[i]]++) { rtamd::set_last_error("rt_render: duplicate row"); return RT_ERR_INVALID_ARG; }
+        }
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         rtamd::set_last_error("rt_render: no HIP device available");
@@ -413,34 +480,47 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     bool secondary = false;
     for (int i = 0; i < d.n_materials; ++i)
         if (d.materials[i].kr > 0.0 || d.materials[i].kt > 0.0) secondary = true;
-    if (d.recursion_limit < 2) secondary = false;
-    const bool deep = cs.max_ivl_depth > 2;   // depth < limit-1 never holds (tracer.cpp:38,51)
+    if (d.recursion_limit < 2) secondary = false;   // depth < limit-1 never holds (tracer.cpp:38,51)
     if (secondary && mode == RT_MODE_STANDARD && d.recursion_limit - 1 > kMaxDepth) {
         rtamd::set_last_error("medium.recursion exceeds the device frame stack (17)");
         return RT_ERR_UNSUPPORTED;
     }
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    Workspace& ws = workspace(dev);
-    std::lock_guard<std::mutex> lk(ws.mu);
+    std::unique_ptr<rt_frame> f(new rt_frame);
+    f->ws = &workspace(dev);
+    f->lock = std::unique_lock<std::mutex>(f->ws->mu);
+    Workspace& ws = *f->ws;
+    f->st = st;
+    f->W = W;
+    f->H = H;
+    f->mode = mode;
+    f->n_rows = n_rows;
+    f->eager = cs.has_eager;
+    f->deep = cs.max_ivl_depth > 2;
+    f->secondary = secondary;
+    f->count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
+    f->rows.assign(rows_host, rows_host + n_rows);
+    f->t_start = t_start;
     if (!ws.ev[0])
         for (int i = 0; i < 4; ++i) HIP_TRY(hipEventCreate(&ws.ev[i]));
 
-    // --- upload the scene (a few KB)
-    std::vector<rt_node> nodes(d.nodes, d.nodes + d.n_nodes);
-    std::vector<rt_material> mats(d.materials, d.materials + d.n_materials);
-    std::vector<rt_light> lights(d.lights, d.lights + d.n_lights);
-    HIP_TRY(upload(ws.nodes, nodes, st));
-    HIP_TRY(upload(ws.mats, mats, st));
-    HIP_TRY(upload(ws.lights, lights, st));
-    HIP_TRY(upload(ws.objs, cs.objs, st));
-    HIP_TRY(upload(ws.ops, cs.ops, st));
-    HIP_TRY(upload(ws.gb, cs.gbounds, st));
+    // --- upload the scene (a few KB; the frame keeps the host copies alive)
+    f->nodes.assign(d.nodes, d.nodes + d.n_nodes);
+    f->mats.assign(d.materials, d.materials + d.n_materials);
+    f->lights.assign(d.lights, d.lights + d.n_lights);
+    f->cs = std::move(cs);
+    HIP_TRY(upload(ws.nodes, f->nodes, st));
+    HIP_TRY(upload(ws.mats, f->mats, st));
+    HIP_TRY(upload(ws.lights, f->lights, st));
+    HIP_TRY(upload(ws.objs, f->cs.objs, st));
+    HIP_TRY(upload(ws.ops, f->cs.ops, st));
+    HIP_TRY(upload(ws.gb, f->cs.gbounds, st));
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
 
-    DevScene S;
+    DevScene& S = f->S;
     S.nodes = ws.nodes.as<rt_node>();
     S.mats = ws.mats.as<rt_material>();
     S.lights = ws.lights.as<rt_light>();
@@ -448,7 +528,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     S.ops = ws.ops.as<DevOp>();
     S.gb = ws.gb.as<float>();
     S.n_lights = d.n_lights;
-    S.n_objs = (int)cs.objs.size();
+    S.n_objs = (int)f->cs.objs.size();
     S.cam_nx = rt_camera_width(&d.camera);
     S.cam_ny = rt_camera_height(&d.camera);
     S.rec_limit = d.recursion_limit;
@@ -462,140 +542,211 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     S.Lx = d.camera.Lx;
     S.Ly = d.camera.Ly;
     S.medium_index = d.medium_index;
-    const bool count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
-    unsigned long long* ctr = ws.counters.as<unsigned long long>();
 
-    uint64_t logical_isect = 0;
-    if (n_rows > 0) {
-        std::vector<int32_t> rows(rows_host, rows_host + n_rows);
-        if (mode == RT_MODE_STANDARD) {
-            int y0 = H, y1 = -1;
-            for (int r : rows) {
-                int y = H - 1 - r;
-                y0 = std::min(y0, y);
-                y1 = std::max(y1, y);
-            }
-            const int64_t q0 = (int64_t)32 * W * y0, q1 = (int64_t)32 * W * (y1 + 1);
-            const int levels = rtamd::mt_levels_needed(kJitterK, q1);
-            if (ws.jplan.levels < levels) {
-                HIP_TRY(hipStreamSynchronize(st));
-                try {
-                    HIP_TRY(ws.jplan.build(kJitterK, levels));
-                } catch (const std::exception& ex) {
-                    rtamd::set_last_error(std::string("jitter plan: ") + ex.what());
-                    return RT_ERR_PROCESSING;
-                }
-            }
-            HIP_TRY(ws.ckpt.ensure(rtamd::mt_ckpt_words(kJitterK, q1) * sizeof(uint32_t)));
-            HIP_TRY(ws.jit.ensure((size_t)(q1 - q0) / 2 * sizeof(double)));
-            HIP_TRY(upload(ws.rows, rows, st));
-            HIP_TRY(hipEventRecord(ws.ev[0], st));
-            HIP_TRY(rtamd::mt_launch_jitter(ws.jplan, q0, q1, ws.ckpt.as<uint32_t>(), ws.jit.as<double>(), st));
-            HIP_TRY(hipEventRecord(ws.ev[1], st));
-            StdParams P;
-            P.W = W;
-            P.H = H;
-            P.n_rows = n_rows;
-            P.jy0 = y0;
-            P.rows = ws.rows.as<int32_t>();
-            P.jit = ws.jit.as<double>();
-            P.fb = fb_dev;
-            P.counters = ctr;
-            dim3 grid((W + 7) / 8, (n_rows + 3) / 4);
-            launch_std(cs.has_eager, deep, secondary, count_ops, grid, st, S, P);
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ws.ev[2], st));
-        } else {
-            // rows needing a primary hit: rendered rows and their vertical neighbours
-            std::vector<char> need(H, 0), shade_row(H, 0);
-            for (int r : rows) {
-                need[r] = 1;
-                shade_row[r] = 1;
-                if (r > 0) need[r - 1] = 1;
-                if (r + 1 < H) need[r + 1] = 1;
-            }
-            std::vector<int32_t> ext, ext_shade, pos(H, -1);
-            for (int r = 0; r < H; ++r)
-                if (need[r]) {
-                    pos[r] = (int)ext.size();
-                    ext.push_back(r);
-                    ext_shade.push_back(shade_row[r]);
-                }
-            std::vector<int32_t> nbr(3 * (size_t)n_rows);
-            for (int i = 0; i < n_rows; ++i) {
-                const int r = rows[i];
-                nbr[3 * i + 0] = r > 0 ? pos[r - 1] : -1;
-                nbr[3 * i + 1] = pos[r];
-                nbr[3 * i + 2] = r + 1 < H ? pos[r + 1] : -1;
-                // logical Scene::intersect calls: trace_paper + centre + valid neighbours
-                logical_isect += (uint64_t)W * 2 + (uint64_t)(W > 1 ? 2 * (W - 1) : 0) +
-                                 (uint64_t)W * ((r > 0) + (r + 1 < H));
-            }
-            const int n_ext = (int)ext.size();
-            std::vector<int32_t> ints;
-            ints.insert(ints.end(), ext.begin(), ext.end());
-            ints.insert(ints.end(), ext_shade.begin(), ext_shade.end());
-            ints.insert(ints.end(), nbr.begin(), nbr.end());
-            ints.insert(ints.end(), rows.begin(), rows.end());
-            HIP_TRY(upload(ws.paper_aux, ints, st));
-            const size_t npx = (size_t)n_ext * W;
-            HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
-            HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
-            PaperParams P;
-            P.W = W;
-            P.H = H;
-            P.n_ext = n_ext;
-            P.n_rows = n_rows;
-            const int32_t* aux = ws.paper_aux.as<int32_t>();
-            P.ext_rows = aux;
-            P.ext_shade = aux + n_ext;
-            P.nbr = aux + 2 * n_ext;
-            P.rows = aux + 2 * n_ext + 3 * (size_t)n_rows;
-            P.hit = ws.paper_i.as<int>();
-            P.mat = P.hit + npx;
-            double* dd = ws.paper_d.as<double>();
-            P.t = dd;
-            P.nx = dd + npx;
-            P.ny = dd + 2 * npx;
-            P.nz = dd + 3 * npx;
-            P.lum = dd + 4 * npx;
-            P.fb = fb_dev;
-            P.counters = ctr;
-            HIP_TRY(hipEventRecord(ws.ev[0], st));
-            HIP_TRY(hipEventRecord(ws.ev[1], st));
-            dim3 g1((W + 15) / 16, (n_ext + 15) / 16);
-            launch_paper(cs.has_eager, deep, count_ops, g1, st, S, P);
-            HIP_TRY(hipGetLastError());
-            dim3 g2((W + 63) / 64, (n_rows + 3) / 4);
-            hipLaunchKernelGGL(k_paper_finish, g2, dim3(256), 0, st, P);
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipEventRecord(ws.ev[2], st));
+    HIP_TRY(hipEventRecord(ws.ev[0], st));
+    if (n_rows > 0 && mode == RT_MODE_STANDARD) {
+        // Loop row y = H-1-rows[ri] consumes outputs [32Wy, 32W(y+1))
+        // (tracer.cpp:284-293).  Jitter rows are laid out in stream order
+        // (jrow = rank of y), so runs of consecutive loop rows - a strip, or
+        // the whole frame - are one range for the generator.
+        const int64_t row_q = (int64_t)32 * W;
+        std::vector<int32_t> order(n_rows);
+        for (int ri = 0; ri < n_rows; ++ri) order[ri] = ri;
+        std::sort(order.begin(), order.end(), [&](int a, int b) { return f->rows[a] > f->rows[b]; });
+        f->rows_jrow.assign(f->rows.begin(), f->rows.end());
+        f->rows_jrow.resize(2 * (size_t)n_rows);
+        ws.jranges.clear();
+        for (int k = 0; k < n_rows; ++k) {
+            const int ri = order[k];
+            f->rows_jrow[n_rows + ri] = k;
+            const int64_t y = H - 1 - f->rows[ri];
+            if (!ws.jranges.empty() && ws.jranges.back().qb == row_q * y)
+                ws.jranges.back().qb += row_q;
+            else
+                ws.jranges.push_back(rtamd::JRange{row_q * y, row_q * (y + 1), (int64_t)k * 16 * W});
         }
-    } else {
-        HIP_TRY(hipEventRecord(ws.ev[0], st));
-        HIP_TRY(hipEventRecord(ws.ev[1], st));
-        HIP_TRY(hipEventRecord(ws.ev[2], st));
+        const int64_t q1 = ws.jranges.back().qb;
+        const int K = jitter_k(row_q * n_rows, q1);
+        rtamd::JitterPlan& plan = ws.jplan[K == kJitterK ? 0 : 1];
+        const int levels = rtamd::mt_levels_needed(K, q1);
+        if (plan.K != K || plan.levels < levels) {
+            try {
+                HIP_TRY(plan.build(K, levels));
+            } catch (const std::exception& ex) {
+                rtamd::set_last_error(std::string("jitter plan: ") + ex.what());
+                return RT_ERR_PROCESSING;
+            }
+        }
+        HIP_TRY(ws.ckpt.ensure(rtamd::mt_ckpt_words(K, q1) * sizeof(uint32_t)));
+        HIP_TRY(ws.jit.ensure((size_t)n_rows * 16 * W * sizeof(double)));
+        HIP_TRY(ws.jscratch.ensure(rtamd::mt_scratch_bytes(K, ws.jranges)));
+        HIP_TRY(upload(ws.rows, f->rows_jrow, st));
+        HIP_TRY(rtamd::mt_launch_jitter(plan, ws.jranges, ws.jjob, ws.jscratch.p, ws.ckpt.as<uint32_t>(),
+                                        ws.jit.as<double>(), st));
+    } else if (n_rows > 0) {
+        // rows needing a primary hit: rendered rows and their vertical neighbours
+        std::vector<char> need(H, 0), shade_row(H, 0);
+        for (int r : f->rows) {
+            need[r] = 1;
+            shade_row[r] = 1;
+            if (r > 0) need[r - 1] = 1;
+            if (r + 1 < H) need[r + 1] = 1;
+        }
+        std::vector<int32_t> ext, ext_shade;
+        f->ext_pos.assign(H, -1);
+        for (int r = 0; r < H; ++r)
+            if (need[r]) {
+                f->ext_pos[r] = (int)ext.size();
+                ext.push_back(r);
+                ext_shade.push_back(shade_row[r]);
+            }
+        std::vector<int32_t> nbr(3 * (size_t)n_rows);
+        for (int i = 0; i < n_rows; ++i) {
+            const int r = f->rows[i];
+            nbr[3 * i + 0] = r > 0 ? f->ext_pos[r - 1] : -1;
+            nbr[3 * i + 1] = f->ext_pos[r];
+            nbr[3 * i + 2] = r + 1 < H ? f->ext_pos[r + 1] : -1;
+            // logical Scene::intersect calls: trace_paper + centre + valid neighbours
+            f->logical_isect += (uint64_t)W * 2 + (uint64_t)(W > 1 ? 2 * (W - 1) : 0) +
+                                (uint64_t)W * ((r > 0) + (r + 1 < H));
+        }
+        f->n_ext = (int)ext.size();
+        f->ext_done.assign(f->n_ext, 0);
+        // aux: ext_rows | ext_shade | nbr | rows | ext lists (n_ext, filled per trace call)
+        f->stage.emplace_back();
+        std::vector<int32_t>& ints = f->stage.back();
+        ints.insert(ints.end(), ext.begin(), ext.end());
+        ints.insert(ints.end(), ext_shade.begin(), ext_shade.end());
+        ints.insert(ints.end(), nbr.begin(), nbr.end());
+        ints.insert(ints.end(), f->rows.begin(), f->rows.end());
+        HIP_TRY(ws.paper_aux.ensure((ints.size() + f->n_ext) * sizeof(int32_t)));
+        HIP_TRY(hipMemcpyAsync(ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        const size_t npx = (size_t)f->n_ext * W;
+        HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
+        HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
     }
+    HIP_TRY(hipEventRecord(ws.ev[1], st));
+    *out = f.release();
+    return RT_OK;
+}
+
+int frame_trace(rt_frame* f, int ri0, int ri1, double* fb) {
+    if (!f) { rtamd::set_last_error("rt_frame_trace: frame is NULL"); return RT_ERR_INVALID_ARG; }
+    if (ri0 < 0 || ri1 < ri0 || ri1 > f->n_rows) { rtamd::set_last_error("rt_frame_trace: bad row range"); return RT_ERR_INVALID_ARG; }
+    if (ri1 == ri0) return RT_OK;
+    if (!fb) { rtamd::set_last_error("rt_frame_trace: fb is NULL"); return RT_ERR_INVALID_ARG; }
+    Workspace& ws = *f->ws;
+    const hipStream_t st = f->st;
+    const int W = f->W, n = ri1 - ri0;
+    unsigned long long* ctr = ws.counters.as<unsigned long long>();
+    if (f->mode == RT_MODE_STANDARD) {
+        StdParams P;
+        P.W = W;
+        P.H = f->H;
+        P.n_rows = n;
+        P.rows = ws.rows.as<int32_t>() + ri0;
+        P.jrow = ws.rows.as<int32_t>() + f->n_rows + ri0;
+        P.jit = ws.jit.as<double>();
+        P.fb = fb;
+        P.counters = ctr;
+        dim3 grid((W + 7) / 8, (n + 3) / 4);
+        launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
+        HIP_TRY(hipGetLastError());
+    } else {
+        // primary hits of the ext rows this chunk reads that no earlier chunk computed
+        std::vector<int32_t> list;
+        for (int i = ri0; i < ri1; ++i) {
+            const int r = f->rows[i];
+            for (int rr = r - 1; rr <= r + 1; ++rr) {
+                if (rr < 0 || rr >= f->H) continue;
+                const int e = f->ext_pos[rr];
+                if (e >= 0 && !f->ext_done[e]) {
+                    f->ext_done[e] = 1;
+                    list.push_back(e);
+                }
+            }
+        }
+        const int32_t* aux = ws.paper_aux.as<int32_t>();
+        const int n_ext = f->n_ext, n_rows = f->n_rows;
+        PaperParams P;
+        P.W = W;
+        P.H = f->H;
+        P.n_ext = n_ext;
+        P.ext_rows = aux;
+        P.ext_shade = aux + n_ext;
+        P.nbr = aux + 2 * n_ext + 3 * (size_t)ri0;
+        P.rows = aux + 2 * n_ext + 3 * (size_t)n_rows + ri0;
+        int32_t* d_list = ws.paper_aux.as<int32_t>() + 2 * n_ext + 4 * (size_t)n_rows + f->list_used;
+        P.ext_list = d_list;
+        P.n_list = (int)list.size();
+        P.n_rows = n;
+        const size_t npx = (size_t)n_ext * W;
+        P.hit = ws.paper_i.as<int>();
+        P.mat = P.hit + npx;
+        double* dd = ws.paper_d.as<double>();
+        P.t = dd;
+        P.nx = dd + npx;
+        P.ny = dd + 2 * npx;
+        P.nz = dd + 3 * npx;
+        P.lum = dd + 4 * npx;
+        P.fb = fb;
+        P.counters = ctr;
+        if (!list.empty()) {
+            f->list_used += (int)list.size();
+            f->stage.push_back(std::move(list));
+            const std::vector<int32_t>& L = f->stage.back();
+            HIP_TRY(hipMemcpyAsync(d_list, L.data(), L.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+            dim3 g1((W + 15) / 16, (P.n_list + 15) / 16);
+            launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
+            HIP_TRY(hipGetLastError());
+        }
+        dim3 g2((W + 63) / 64, (n + 3) / 4);
+        hipLaunchKernelGGL(k_paper_finish, g2, dim3(256), 0, st, P);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(ws.ev[2], st));
+    f->traced = true;
+    return RT_OK;
+}
+
+int frame_end(rt_frame* f, rt_stats* stats) {
+    if (!f) { rtamd::set_last_error("rt_frame_end: frame is NULL"); return RT_ERR_INVALID_ARG; }
+    std::unique_ptr<rt_frame> own(f);
+    Workspace& ws = *f->ws;
+    const hipStream_t st = f->st;
+    if (!f->traced) HIP_TRY(hipEventRecord(ws.ev[2], st));
+    const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     std::vector<unsigned long long> slots((size_t)kCounterSlots * kCounterWords);
-    HIP_TRY(hipMemcpyAsync(slots.data(), ctr, ctr_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(slots.data(), ws.counters.p, ctr_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     unsigned long long hc[kCounterWords] = {};
     for (int sl = 0; sl < kCounterSlots; ++sl)
         for (int k = 0; k < kCounterWords; ++k) hc[k] += slots[(size_t)sl * kCounterWords + k];
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
-        stats->rays_intersect = mode == RT_MODE_PAPER ? logical_isect : hc[0];
+        stats->rays_intersect = f->mode == RT_MODE_PAPER ? f->logical_isect : hc[0];
         stats->rays_occluded = hc[1];
         stats->rays_traced = hc[0] + hc[1];
-        stats->pixels = (uint64_t)n_rows * W;
+        stats->pixels = (uint64_t)f->n_rows * f->W;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, ws.ev[0], ws.ev[1]) == hipSuccess) stats->ms_rng = ms;
         if (hipEventElapsedTime(&ms, ws.ev[1], ws.ev[2]) == hipSuccess) stats->ms_kernel = ms;
         for (int k = 0; k < 16; ++k) stats->ops[k] = hc[2 + k];
         stats->ms_total =
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f->t_start).count();
     }
     return RT_OK;
+}
+
+int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
+                     double* fb_dev, hipStream_t st, rt_stats* stats) {
+    if (n_rows > 0 && !fb_dev) { rtamd::set_last_error("rt_render: bad rows/fb"); return RT_ERR_INVALID_ARG; }
+    rt_frame* f = nullptr;
+    int rc = frame_begin(s, W, H, mode, flags, rows_host, n_rows, st, &f);
+    if (rc != RT_OK) return rc;
+    rc = frame_trace(f, 0, n_rows, fb_dev);
+    const int rc2 = frame_end(f, stats);
+    return rc != RT_OK ? rc : rc2;
 }
 
 }  // namespace
@@ -611,6 +762,17 @@ extern "C" int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, 
                                      int n_rows, double* fb_rows_dev, void* hip_stream, rt_stats* stats) {
     return render_rows_impl(s, W, H, mode, flags, rows_host, n_rows, fb_rows_dev, (hipStream_t)hip_stream, stats);
 }
+
+extern "C" int rt_frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host,
+                              int n_rows, void* hip_stream, rt_frame** out) {
+    return frame_begin(s, W, H, mode, flags, rows_host, n_rows, (hipStream_t)hip_stream, out);
+}
+
+extern "C" int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev) {
+    return frame_trace(f, ri0, ri1, fb_rows_dev);
+}
+
+extern "C" int rt_frame_end(rt_frame* f, rt_stats* stats) { return frame_end(f, stats); }
 
 extern "C" int rt_render(const rt_scene* s, int W, int H, int mode, int flags, double* fb_host, rt_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -692,23 +854,28 @@ extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
     }
 }
 
-extern "C" int rt_test_jitter_device(int64_t q0, int64_t q1, int64_t first, int64_t count, double* out_host) {
-    if (q0 < 0 || q1 <= q0 || (q0 & 1) || (q1 & 1) || !out_host || first * 2 < q0 || (first + count) * 2 > q1)
+extern "C" int rt_test_jitter_device(int K, int64_t q0, int64_t q1, int64_t first, int64_t count,
+                                     double* out_host) {
+    if (K <= 0 || q0 < 0 || q1 <= q0 || (q0 & 1) || (q1 & 1) || !out_host || first * 2 < q0 || (first + count) * 2 > q1)
         return RT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
     rtamd::JitterPlan plan;
-    HIP_TRY(plan.build(kJitterK, rtamd::mt_levels_needed(kJitterK, q1)));
-    DBuf dc, dj;
-    HIP_TRY(dc.ensure(rtamd::mt_ckpt_words(kJitterK, q1) * 4));
+    HIP_TRY(plan.build(K, rtamd::mt_levels_needed(K, q1)));
+    DBuf dc, dj, ds;
+    const std::vector<rtamd::JRange> ranges{rtamd::JRange{q0, q1, 0}};
+    rtamd::JitterJob job;
+    HIP_TRY(dc.ensure(rtamd::mt_ckpt_words(K, q1) * 4));
     HIP_TRY(dj.ensure((size_t)(q1 - q0) / 2 * sizeof(double)));
-    HIP_TRY(rtamd::mt_launch_jitter(plan, q0, q1, dc.as<uint32_t>(), dj.as<double>(), nullptr));
+    HIP_TRY(ds.ensure(rtamd::mt_scratch_bytes(K, ranges)));
+    HIP_TRY(rtamd::mt_launch_jitter(plan, ranges, job, ds.p, dc.as<uint32_t>(), dj.as<double>(), nullptr));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out_host, dj.as<double>() + (first - q0 / 2), (size_t)count * sizeof(double),
                       hipMemcpyDeviceToHost));
     plan.release();
     (void)hipFree(dc.p);
     (void)hipFree(dj.p);
+    (void)hipFree(ds.p);
     return RT_OK;
 }
 

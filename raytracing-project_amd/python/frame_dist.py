@@ -31,3 +31,61 @@ def gather_row_index(H: int, world: int, strip: int = STRIP) -> list[int]:
         rr = strip_rows(H, r, world, strip)
         out.extend(rr + [-1] * (m - len(rr)))
     return out
+
+
+def chunk_bounds(m: int, chunks: int) -> list[tuple[int, int]]:
+    """Split the padded per-rank row list [0, m) into `chunks` contiguous
+    pieces (the pipeline units: chunk k is gathered while k+1 is traced)."""
+    chunks = max(1, min(chunks, m)) if m > 0 else 1
+    out = [(k * m // chunks, (k + 1) * m // chunks) for k in range(chunks)]
+    return [(a, b) for a, b in out if b > a] or [(0, 0)]
+
+
+class DistFrame:
+    """One rank's share of a W x H frame and the buffers of its gather.
+
+    rows        output rows this rank renders (interleaved strips)
+    mine        [m, W, 3] float64 rows of this rank, padded to m = max_rows
+    stage/full  rank 0: [world, m, W, 3] gather target and the [H, W, 3] frame
+    slot_rows   rank 0: destination row of every stage slot (-1 = pad)
+
+    run() traces chunk k of `mine` and immediately hands it to an async
+    gather to rank 0 (one collective per chunk, on the backend's own stream:
+    RCCL over xGMI on the GPU, gloo in the CPU tests), so transfers overlap
+    the tracing of later chunks; rank 0 then scatters the slots into `full`.
+    With world == 1 `mine` already is the frame (rows 0..H-1 in order)."""
+
+    def __init__(self, W: int, H: int, rank: int, world: int, device, chunks: int = 4, strip: int = STRIP):
+        import torch
+
+        self.W, self.H, self.rank, self.world = W, H, rank, world
+        self.rows = strip_rows(H, rank, world, strip)
+        self.m = max_rows(H, world, strip)
+        self.bounds = chunk_bounds(self.m, chunks if world > 1 else 1)
+        self.mine = torch.zeros((self.m, W, 3), dtype=torch.float64, device=device)
+        self.stage = self.full = self.slot_rows = None
+        if world > 1 and rank == 0:
+            self.stage = torch.zeros((world, self.m, W, 3), dtype=torch.float64, device=device)
+            self.full = torch.zeros((H, W, 3), dtype=torch.float64, device=device)
+            self.slot_rows = torch.tensor(gather_row_index(H, world, strip), dtype=torch.int32, device=device)
+        elif world == 1:
+            self.full = self.mine
+
+    def run(self, trace_chunk, dist=None, scatter=None):
+        """trace_chunk(a, b, out) renders list entries [a, b) of self.rows into
+        out = self.mine[a:b] (may be asynchronous on the current stream);
+        scatter(stage, slot_rows, full) places the gathered slots (rank 0)."""
+        n = len(self.rows)
+        works = []
+        for a, b in self.bounds:
+            hi = min(b, n)
+            if hi > a:
+                trace_chunk(a, hi, self.mine[a:hi])
+            if self.world > 1:
+                gl = [self.stage[r, a:b] for r in range(self.world)] if self.rank == 0 else None
+                works.append(dist.gather(self.mine[a:b], gather_list=gl, dst=0, async_op=True))
+        for w in works:
+            w.wait()
+        if self.world > 1 and self.rank == 0:
+            scatter(self.stage, self.slot_rows, self.full)
+        return self.full

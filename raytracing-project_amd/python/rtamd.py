@@ -32,6 +32,9 @@ ORACLE_DIR = os.path.join(REPO_DIR, "oracle")
 RT_OK = 0
 RT_MODE_STANDARD = 0
 RT_MODE_PAPER = 1
+RT_OK = 0
+RT_ERR_INVALID_ARG = -1
+RT_ERR_NO_DEVICE = -7
 RT_FLAG_NONE = 0
 RT_FLAG_COUNT_OPS = 1
 RT_FLAG_NO_CULL = 2
@@ -143,6 +146,11 @@ def amd_lib():
                                               C.POINTER(C.c_int32), C.c_int, C.c_void_p, C.c_void_p,
                                               C.POINTER(Stats)]
         lib.rt_scatter_rows_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        if hasattr(lib, "rt_frame_begin"):   # (absent only in RTAMD_LIB builds of older sources)
+            lib.rt_frame_begin.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32),
+                                           C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
+            lib.rt_frame_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+            lib.rt_frame_end.argtypes = [C.c_void_p, C.POINTER(Stats)]
         lib.rt_framebuffer_to_rgb8_device.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
         lib.rt_device_count.restype = C.c_int
         _amd = lib

@@ -2,8 +2,9 @@
 
 Each rank renders its interleaved row strips (standard mode: every strip
 starts its own mt19937 stream offset; paper mode: neighbour rows outside the
-strip are re-traced), the padded row buffers are all_gathered exactly as
-bench.py does with RCCL, and rank 0 scatters them into the frame.  The
+strip are re-traced), the padded row buffers go through frame_dist.DistFrame — the same chunked
+gather-to-rank-0 pipeline bench.py runs over RCCL — and rank 0 scatters
+them into the frame.  The
 per-rank renderer here is the CPU oracle (test infrastructure), so this test
 pins the partition / offset / gather / scatter logic, not the GPU kernels
 (tests/test_gpu_jitter_rows.py covers rt_render_rows_device on the GPU)."""
@@ -39,21 +40,22 @@ def _worker(rank, world, port, text, mode, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
-    rows = frame_dist.strip_rows(H, rank, world)
-    m = frame_dist.max_rows(H, world)
-    mine = np.zeros((m, W, 3))
-    for k, r in enumerate(rows):   # render row by row to exercise arbitrary offsets
-        fb, _ = rtamd.oracle_render(sc, W, H, mode, r, r + 1)
-        mine[k] = fb[0]
-    buf = torch.zeros((world * m, W, 3), dtype=torch.float64)
-    dist.all_gather_into_tensor(buf, torch.from_numpy(mine))
+    df = frame_dist.DistFrame(W, H, rank, world, "cpu", chunks=3)
+
+    def trace_chunk(a, b, out):   # row by row: arbitrary stream offsets
+        for k in range(a, b):
+            r = df.rows[k]
+            fb, _ = rtamd.oracle_render(sc, W, H, mode, r, r + 1)
+            out[k - a] = torch.from_numpy(fb[0])
+
+    def scatter(stage, slot_rows, full):
+        flat = stage.reshape(-1, W, 3)
+        keep = slot_rows >= 0
+        full[slot_rows[keep].long()] = flat[keep]
+
+    frame = df.run(trace_chunk, dist, scatter)
     if rank == 0:
-        idx = frame_dist.gather_row_index(H, world)
-        frame = np.zeros((H, W, 3))
-        for slot, r in enumerate(idx):
-            if r >= 0:
-                frame[r] = buf[slot].numpy()
-        np.save(out_path, frame)
+        np.save(out_path, frame.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -81,3 +83,8 @@ def test_strip_partition_covers_frame():
             idx = frame_dist.gather_row_index(H, world)
             assert len(idx) == world * frame_dist.max_rows(H, world)
             assert sorted(r for r in idx if r >= 0) == list(range(H))
+            m = frame_dist.max_rows(H, world)
+            for chunks in (1, 3, 4, 64):
+                b = frame_dist.chunk_bounds(m, chunks)
+                assert b[0][0] == 0 and b[-1][1] == m
+                assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))

@@ -16,13 +16,14 @@ FRAME_4K = 32 * 3840 * 2160
 FRAME_8K = 32 * 7680 * 4320
 
 
-def _device_draws(q0, q1, first, count):
+def _device_draws(q0, q1, first, count, K=1024):
     import rtamd
 
     lib = rtamd.amd_lib()
-    lib.rt_test_jitter_device.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int64, C.POINTER(C.c_double)]
+    lib.rt_test_jitter_device.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                          C.POINTER(C.c_double)]
     out = np.zeros(count)
-    rc = lib.rt_test_jitter_device(q0, q1, first, count, out.ctypes.data_as(C.POINTER(C.c_double)))
+    rc = lib.rt_test_jitter_device(K, q0, q1, first, count, out.ctypes.data_as(C.POINTER(C.c_double)))
     assert rc == 0, rtamd.last_error()
     return out
 
@@ -50,6 +51,17 @@ def test_jitter_stream_matches_serial(gpu, q0, q1, first, count):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K", [256, 512])
+@pytest.mark.parametrize("q0,q1,first,count", [
+    (0, 40 * SEG, 0, 2048),
+    (FRAME_4K - 32 * 3840 * 8, FRAME_4K, FRAME_4K // 2 - 16 * 3840 * 8, 16 * 3840 * 8),   # last strip of 4K
+])
+def test_jitter_stream_short_segments(gpu, K, q0, q1, first, count):
+    """The multi-GPU segment lengths (more checkpoints, one more tree level)."""
+    assert np.array_equal(_device_draws(q0, q1, first, count, K), _oracle_draws(first, count))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1])
 def test_row_subset_matches_full_frame(gpu, mode):
     """rt_render_rows_device on interleaved 8-row strips (the multi-GPU split)
@@ -63,7 +75,7 @@ def test_row_subset_matches_full_frame(gpu, mode):
     W, H = sc.width, sc.height
     full = rt.Tracer(sc, W, H, mode).render()
     lib = rt.amd_lib()
-    for world in (2, 3):
+    for world in (2, 3, 5):
         for rank in range(world):
             rows = [r for s in range((H + 7) // 8) if s % world == rank for r in range(s * 8, min(H, s * 8 + 8))]
             buf = torch.zeros((len(rows), W, 3), dtype=torch.float64, device="cuda")
@@ -73,3 +85,31 @@ def test_row_subset_matches_full_frame(gpu, mode):
             torch.cuda.synchronize()
             got = buf.cpu().numpy()
             assert np.array_equal(got, full[rows]), (world, rank)
+
+
+@pytest.mark.gpu
+def test_unordered_row_subset_and_duplicates(gpu):
+    """Rows in arbitrary order (jitter ranges sorted on the host, written to
+    their own jitter row) match the full frame; a duplicated row is rejected."""
+    import torch
+
+    import scenes
+    rt = gpu
+    text, _ = scenes.config_json(4, dpi=40)
+    sc = rt.load_scene_from_json_text(text)
+    W, H = sc.width, sc.height
+    full = rt.Tracer(sc, W, H, 0).render()
+    lib = rt.amd_lib()
+    rng = np.random.default_rng(7)
+    rows = [int(r) for r in rng.permutation(H)[: H // 3]]
+    buf = torch.zeros((len(rows), W, 3), dtype=torch.float64, device="cuda")
+    rc = lib.rt_render_rows_device(sc.handle, W, H, 0, 0, (C.c_int32 * len(rows))(*rows), len(rows),
+                                   C.c_void_p(buf.data_ptr()), None, None)
+    assert rc == 0, rt.last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), full[rows])
+    dup = rows[:4] + rows[:1]
+    rc = lib.rt_render_rows_device(sc.handle, W, H, 0, 0, (C.c_int32 * len(dup))(*dup), len(dup),
+                                   C.c_void_p(buf.data_ptr()), None, None)
+    assert rc == rt.RT_ERR_INVALID_ARG
+    assert "duplicate" in rt.last_error()
