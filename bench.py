@@ -90,10 +90,12 @@ def main() -> int:
     n_rows = len(rows)
     rows_c = (C.c_int32 * max(1, n_rows))(*rows)
     stream = torch.cuda.current_stream(dev)
+    # chunks alternate between two streams so one chunk's launch tail overlaps the next chunk
+    streams = [stream, torch.cuda.Stream(dev)]
     st = rtamd.Stats()
 
-    def scatter(stage, slot_rows, full):
-        rc = lib.rt_scatter_rows_device(C.c_void_p(stage.data_ptr()), C.c_void_p(slot_rows.data_ptr()),
+    def scatter(src, slot_rows, full):
+        rc = lib.rt_scatter_rows_device(C.c_void_p(src.data_ptr()), C.c_void_p(slot_rows.data_ptr()),
                                         slot_rows.numel(), W, C.c_void_p(full.data_ptr()),
                                         C.c_void_p(stream.cuda_stream))
         if rc != 0:
@@ -110,13 +112,13 @@ def main() -> int:
             raise RuntimeError(f"rt_frame_begin failed ({rc}): {rtamd.last_error()}")
         err = []
 
-        def trace_chunk(a, b, out):
-            r = lib.rt_frame_trace(fr, a, b, C.c_void_p(out.data_ptr()))
+        def trace_chunk(a, b, out, s):
+            r = lib.rt_frame_trace(fr, a, b, C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream))
             if r != 0:
                 err.append((r, rtamd.last_error()))
 
         try:
-            df.run(trace_chunk, dist, scatter)
+            df.run(trace_chunk, dist, scatter, streams)
         finally:
             rc = lib.rt_frame_end(fr, C.byref(stats))
         if err or rc != 0:

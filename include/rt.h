@@ -220,15 +220,17 @@ int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, int flags,
  * (SURVEY.md §8e).  rt_frame_begin validates the rows (as
  * rt_render_rows_device), uploads the scene and enqueues the jitter stream of
  * ALL the listed rows; rt_frame_trace enqueues the trace of list entries
- * [ri0, ri1) into fb_rows_dev[0 .. ri1-ri0) (each list entry traced once);
- * rt_frame_end waits for the stream, fills stats and frees the frame — call
- * it exactly once per begun frame, also after an error.  begin/trace only
- * enqueue work on hip_stream.  One frame per device at a time (begin blocks
- * while another frame of the same device is open). */
+ * [ri0, ri1) into fb_rows_dev[0 .. ri1-ri0) (each list entry traced once)
+ * on trace_stream (NULL = the frame's stream; another stream first waits for
+ * begin's work, so consecutive chunks on two streams overlap their launch
+ * tails); rt_frame_end joins every stream used, waits, fills stats and frees
+ * the frame — call it exactly once per begun frame, also after an error.
+ * begin/trace only enqueue work.  One frame per device at a time (begin
+ * blocks while another frame of the same device is open). */
 typedef struct rt_frame rt_frame;
 int rt_frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
                    void* hip_stream, rt_frame** out);
-int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev);
+int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev, void* trace_stream);
 int rt_frame_end(rt_frame* f, rt_stats* stats);
 
 /* fb_dev[rows[i]][*] = src_dev[i][*] for i < n_rows (device copy, W*3 doubles per row);

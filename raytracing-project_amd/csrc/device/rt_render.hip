@@ -393,6 +393,7 @@ struct Workspace {
     rtamd::JitterJob jjob;
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
 };
 
 Workspace& workspace(int dev) {
@@ -435,6 +436,8 @@ struct rt_frame {
     std::vector<int32_t> ext_pos;              // output row -> ext index (-1: none)
     std::vector<char> ext_done;                // primary hit already launched
     int list_used = 0;                         // ext-list entries consumed in the aux buffer
+    int n_tev = 0;                             // trace events recorded (ws.tev[0 .. n_tev))
+    hipStream_t last_st = nullptr;             // stream of the previous trace call
     std::vector<std::vector<int32_t>> stage;   // host sources of async uploads
     rtamd::CompiledScene cs;
     std::vector<rt_node> nodes;
@@ -630,15 +633,21 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     return RT_OK;
 }
 
-int frame_trace(rt_frame* f, int ri0, int ri1, double* fb) {
+int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
     if (!f) { rtamd::set_last_error("rt_frame_trace: frame is NULL"); return RT_ERR_INVALID_ARG; }
     if (ri0 < 0 || ri1 < ri0 || ri1 > f->n_rows) { rtamd::set_last_error("rt_frame_trace: bad row range"); return RT_ERR_INVALID_ARG; }
     if (ri1 == ri0) return RT_OK;
     if (!fb) { rtamd::set_last_error("rt_frame_trace: fb is NULL"); return RT_ERR_INVALID_ARG; }
     Workspace& ws = *f->ws;
-    const hipStream_t st = f->st;
+    const hipStream_t st = hs ? hs : f->st;
     const int W = f->W, n = ri1 - ri0;
     unsigned long long* ctr = ws.counters.as<unsigned long long>();
+    // another stream first waits for the scene upload and jitter (begin); in
+    // paper mode a chunk also reads primary hits an earlier chunk computed,
+    // so chunks on different streams are chained
+    if (st != f->st) HIP_TRY(hipStreamWaitEvent(st, ws.ev[1], 0));
+    if (f->mode == RT_MODE_PAPER && f->n_tev > 0 && f->last_st != st)
+        HIP_TRY(hipStreamWaitEvent(st, ws.tev[f->n_tev - 1], 0));
     if (f->mode == RT_MODE_STANDARD) {
         StdParams P;
         P.W = W;
@@ -704,7 +713,14 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb) {
         hipLaunchKernelGGL(k_paper_finish, g2, dim3(256), 0, st, P);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(ws.ev[2], st));
+    if ((int)ws.tev.size() <= f->n_tev) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ws.tev.push_back(e);
+    }
+    HIP_TRY(hipEventRecord(ws.tev[f->n_tev], st));
+    ++f->n_tev;
+    f->last_st = st;
     f->traced = true;
     return RT_OK;
 }
@@ -714,7 +730,8 @@ int frame_end(rt_frame* f, rt_stats* stats) {
     std::unique_ptr<rt_frame> own(f);
     Workspace& ws = *f->ws;
     const hipStream_t st = f->st;
-    if (!f->traced) HIP_TRY(hipEventRecord(ws.ev[2], st));
+    for (int i = 0; i < f->n_tev; ++i) HIP_TRY(hipStreamWaitEvent(st, ws.tev[i], 0));   // join trace streams
+    HIP_TRY(hipEventRecord(ws.ev[2], st));
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     std::vector<unsigned long long> slots((size_t)kCounterSlots * kCounterWords);
     HIP_TRY(hipMemcpyAsync(slots.data(), ws.counters.p, ctr_bytes, hipMemcpyDeviceToHost, st));
@@ -744,7 +761,7 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     rt_frame* f = nullptr;
     int rc = frame_begin(s, W, H, mode, flags, rows_host, n_rows, st, &f);
     if (rc != RT_OK) return rc;
-    rc = frame_trace(f, 0, n_rows, fb_dev);
+    rc = frame_trace(f, 0, n_rows, fb_dev, nullptr);
     const int rc2 = frame_end(f, stats);
     return rc != RT_OK ? rc : rc2;
 }
@@ -768,8 +785,8 @@ extern "C" int rt_frame_begin(const rt_scene* s, int W, int H, int mode, int fla
     return frame_begin(s, W, H, mode, flags, rows_host, n_rows, (hipStream_t)hip_stream, out);
 }
 
-extern "C" int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev) {
-    return frame_trace(f, ri0, ri1, fb_rows_dev);
+extern "C" int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev, void* hip_stream) {
+    return frame_trace(f, ri0, ri1, fb_rows_dev, (hipStream_t)hip_stream);
 }
 
 extern "C" int rt_frame_end(rt_frame* f, rt_stats* stats) { return frame_end(f, stats); }

@@ -71,21 +71,36 @@ class DistFrame:
         elif world == 1:
             self.full = self.mine
 
-    def run(self, trace_chunk, dist=None, scatter=None):
-        """trace_chunk(a, b, out) renders list entries [a, b) of self.rows into
-        out = self.mine[a:b] (may be asynchronous on the current stream);
-        scatter(stage, slot_rows, full) places the gathered slots (rank 0)."""
+    def run(self, trace_chunk, dist=None, scatter=None, streams=None):
+        """trace_chunk(a, b, out, stream) renders list entries [a, b) of
+        self.rows into out = self.mine[a:b] (may be asynchronous on `stream`);
+        scatter(src, slot_rows, full) places gathered slots src[i] at row
+        slot_rows[i] of full (rank 0; -1 = padding, skipped).
+        With `streams` (torch.cuda.Stream list) chunk k is traced and its
+        gather issued on streams[k % len], so consecutive chunks overlap
+        their launch tails; the caller joins them (rt_frame_end)."""
+        import contextlib
+
         n = len(self.rows)
         works = []
-        for a, b in self.bounds:
+        for k, (a, b) in enumerate(self.bounds):
+            s = streams[k % len(streams)] if streams else None
             hi = min(b, n)
             if hi > a:
-                trace_chunk(a, hi, self.mine[a:hi])
+                trace_chunk(a, hi, self.mine[a:hi], s)
             if self.world > 1:
+                import torch
+
                 gl = [self.stage[r, a:b] for r in range(self.world)] if self.rank == 0 else None
-                works.append(dist.gather(self.mine[a:b], gather_list=gl, dst=0, async_op=True))
-        for w in works:
+                with torch.cuda.stream(s) if s is not None else contextlib.nullcontext():
+                    works.append(dist.gather(self.mine[a:b], gather_list=gl, dst=0, async_op=True))
+        # rank 0: place chunk k as soon as its gather is in (the wait orders the
+        # current stream after the collective); all but the last chunk's
+        # scatter overlap the remaining traces
+        for k, w in enumerate(works):
             w.wait()
-        if self.world > 1 and self.rank == 0:
-            scatter(self.stage, self.slot_rows, self.full)
+            if self.rank == 0:
+                a, b = self.bounds[k]
+                for r in range(self.world):
+                    scatter(self.stage[r, a:b], self.slot_rows[r * self.m + a:r * self.m + b], self.full)
         return self.full

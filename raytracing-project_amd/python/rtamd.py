@@ -149,7 +149,7 @@ def amd_lib():
         if hasattr(lib, "rt_frame_begin"):   # (absent only in RTAMD_LIB builds of older sources)
             lib.rt_frame_begin.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32),
                                            C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
-            lib.rt_frame_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+            lib.rt_frame_trace.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
             lib.rt_frame_end.argtypes = [C.c_void_p, C.POINTER(Stats)]
         lib.rt_framebuffer_to_rgb8_device.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
         lib.rt_device_count.restype = C.c_int

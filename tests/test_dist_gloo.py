@@ -42,16 +42,15 @@ def _worker(rank, world, port, text, mode, out_path):
     W, H = sc.width, sc.height
     df = frame_dist.DistFrame(W, H, rank, world, "cpu", chunks=3)
 
-    def trace_chunk(a, b, out):   # row by row: arbitrary stream offsets
+    def trace_chunk(a, b, out, stream):   # row by row: arbitrary stream offsets
         for k in range(a, b):
             r = df.rows[k]
             fb, _ = rtamd.oracle_render(sc, W, H, mode, r, r + 1)
             out[k - a] = torch.from_numpy(fb[0])
 
-    def scatter(stage, slot_rows, full):
-        flat = stage.reshape(-1, W, 3)
+    def scatter(src, slot_rows, full):
         keep = slot_rows >= 0
-        full[slot_rows[keep].long()] = flat[keep]
+        full[slot_rows[keep].long()] = src[keep]
 
     frame = df.run(trace_chunk, dist, scatter)
     if rank == 0:

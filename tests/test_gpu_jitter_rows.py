@@ -113,3 +113,42 @@ def test_unordered_row_subset_and_duplicates(gpu):
                                    C.c_void_p(buf.data_ptr()), None, None)
     assert rc == rt.RT_ERR_INVALID_ARG
     assert "duplicate" in rt.last_error()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_frame_chunks_on_two_streams(gpu, mode):
+    """rt_frame_begin / trace (chunks alternating between two HIP streams) /
+    end reproduces the rows of the full frame bit for bit, with the same ray
+    counts as one rt_render_rows_device call (the bench's multi-GPU path)."""
+    import torch
+
+    import frame_dist
+    import scenes
+    rt = gpu
+    text, _ = scenes.config_json(4, dpi=40)
+    sc = rt.load_scene_from_json_text(text)
+    W, H = sc.width, sc.height
+    full = rt.Tracer(sc, W, H, mode).render()
+    lib = rt.amd_lib()
+    rows = frame_dist.strip_rows(H, 1, 3)
+    s0 = torch.cuda.current_stream()
+    streams = [s0, torch.cuda.Stream()]
+    buf = torch.zeros((len(rows), W, 3), dtype=torch.float64, device="cuda")
+    fr = C.c_void_p()
+    rc = lib.rt_frame_begin(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
+                            C.c_void_p(s0.cuda_stream), C.byref(fr))
+    assert rc == 0, rt.last_error()
+    for k, (a, b) in enumerate(frame_dist.chunk_bounds(len(rows), 5)):
+        rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf[a].data_ptr()), C.c_void_p(streams[k % 2].cuda_stream))
+        assert rc == 0, rt.last_error()
+    st = rt.Stats()
+    assert lib.rt_frame_end(fr, C.byref(st)) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), full[rows])
+    st1 = rt.Stats()
+    buf2 = torch.zeros_like(buf)
+    rc = lib.rt_render_rows_device(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
+                                   C.c_void_p(buf2.data_ptr()), None, C.byref(st1))
+    assert rc == 0
+    assert (st.rays_intersect, st.rays_occluded) == (st1.rays_intersect, st1.rays_occluded)

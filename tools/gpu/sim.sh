@@ -3,8 +3,9 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
 : > gpurun_out/sim.log
-for K in 0; do
-timeout -k 10 300 python tools/sim_ranks.py --worlds 1,2,4,8 >> gpurun_out/sim.log 2>&1 || { echo sim failed; tail gpurun_out/sim.log; exit 1; }
-echo "K=$K done" >> gpurun_out/sim.log
+timeout -k 10 300 python tools/sim_ranks.py --worlds 1,8 >> gpurun_out/sim.log 2>&1 || { echo sim failed; tail gpurun_out/sim.log; exit 1; }
+for c in 2 4 8; do
+timeout -k 10 300 python tools/sim_ranks.py --worlds 8 --chunks $c >> gpurun_out/sim.log 2>&1 || { echo sim failed; tail gpurun_out/sim.log; exit 1; }
+timeout -k 10 300 python tools/sim_ranks.py --worlds 8 --chunks $c --two-streams >> gpurun_out/sim.log 2>&1 || { echo sim failed; tail gpurun_out/sim.log; exit 1; }
 done
-cat gpurun_out/sim.log
+grep world gpurun_out/sim.log

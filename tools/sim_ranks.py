@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--strip", type=int, default=frame_dist.STRIP)
     ap.add_argument("--chunks", type=int, default=1, help="trace through rt_frame_* in this many chunks")
+    ap.add_argument("--two-streams", action="store_true", help="alternate chunks between two streams")
     args = ap.parse_args()
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
@@ -40,6 +41,7 @@ def main():
     lib = rtamd.amd_lib()
     buf = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     stream = torch.cuda.current_stream()
+    streams = [stream, torch.cuda.Stream()] if args.two_streams else [stream]
     st = rtamd.Stats()
 
     def run(rows):
@@ -52,8 +54,9 @@ def main():
         rc = lib.rt_frame_begin(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
                                 C.c_void_p(stream.cuda_stream), C.byref(fr))
         assert rc == 0, rtamd.last_error()
-        for a, b in frame_dist.chunk_bounds(len(rows), args.chunks):
-            rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf[a].data_ptr()))
+        for k, (a, b) in enumerate(frame_dist.chunk_bounds(len(rows), args.chunks)):
+            s = streams[k % len(streams)]
+            rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf[a].data_ptr()), C.c_void_p(s.cuda_stream))
             assert rc == 0, rtamd.last_error()
         rc = lib.rt_frame_end(fr, C.byref(st))
         assert rc == 0, rtamd.last_error()
@@ -78,7 +81,7 @@ def main():
         worst = max(p["wall_ms"] for p in per)
         if base is None and N == 1:
             base = worst
-        out = {"config": args.config, "world": N, "strip": args.strip, "chunks": args.chunks, "max_rank_wall_ms": round(worst, 3),
+        out = {"config": args.config, "world": N, "strip": args.strip, "chunks": args.chunks, "two_streams": args.two_streams, "max_rank_wall_ms": round(worst, 3),
                "max_rank_rng_ms": round(max(p["rng_ms"] for p in per), 3),
                "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
                "min_rank_kernel_ms": round(min(p["kernel_ms"] for p in per), 3),
