@@ -55,3 +55,30 @@ def test_no_cull_flag_same_image(gpu):
     a = gpu.Tracer(sc, sc.width, sc.height, 0).render()
     b = gpu.Tracer(sc, sc.width, sc.height, 0, flags=gpu.RT_FLAG_NO_CULL).render()
     assert np.array_equal(a, b)
+
+
+# Counters of the FLOP model (bench.py model_flops).  With
+# culling off, the standard-mode kernels execute the reference's primitive
+# tests one for one; two counters legitimately differ: Pokeball regions are
+# resolved only for the winning hit (lazy hit references) and eager
+# (transform-inside-CSG) programs re-run once for the winner.
+FLOP_COUNTERS = ["sphere_isect", "sphere_isect_hit", "sphere_ivl", "sphere_ivl_hit", "half_isect", "half_isect_hit",
+                 "half_ivl", "xform", "shade_light", "shade_spec", "secondary", "light_eval", "shade_call"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg2", "cfg4", "cfg5", "penguin", "snorlax", "csg_ops", "reflect_refract",
+                                  "rotation_scaling", "inside_camera", "halfspace_in_csg"])
+def test_opcounts_match_reference_without_cull(gpu, name):
+    """bench.py prices roofline.achieved with these counts: they must be the
+    reference's own (the oracle counts every Primitive call it restates)."""
+    rt = gpu
+    sc = rt.load_scene_from_json_text(SMALL[name]())
+    W, H = sc.width, sc.height
+    st = rt.Stats()
+    rt.Tracer(sc, W, H, 0, flags=rt.RT_FLAG_COUNT_OPS | rt.RT_FLAG_NO_CULL).render(st)
+    _, ost = rt.oracle_render(sc, W, H, 0, threads=8)
+    g = {n: int(st.ops[i]) for i, n in enumerate(rt.OP_NAMES)}
+    o = {n: int(ost.ops[i]) for i, n in enumerate(rt.OP_NAMES)}
+    assert {n: g[n] for n in FLOP_COUNTERS} == {n: o[n] for n in FLOP_COUNTERS}
+    assert (st.rays_intersect, st.rays_occluded) == (ost.rays_intersect, ost.rays_occluded)
