@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -34,24 +35,26 @@ namespace {
 
 constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
 constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics
-constexpr int kJitterK = 1024;          // twist blocks per jitter segment (whole frames)
-constexpr int kJitterKSmall = 512;      // ... for row subsets (multi-GPU ranks)
+constexpr int kJitterKMax = 1024;       // twist blocks per jitter segment, upper bound
+constexpr int kJitterKMin = 64;
 
-// Segment length for a jitter job: a segment is regenerated serially by one
-// workgroup (latency ~ K twist blocks), a checkpoint costs one GF(2) jump
-// (~10k-tap correlation over 20k words in LDS).  Whole frames amortise the
-// jumps with long segments; a rank that needs a fraction of the stream has
-// fewer checkpoints to jump to, so shorter segments cut its fill latency.
-// RT_JITTER_K overrides (diagnostics).
-int jitter_k(int64_t words_needed, int64_t q_max) {
+// Segment length for a jitter job.  A segment is regenerated serially by one
+// workgroup (latency ~ K twist blocks, ~0.6 us each); a checkpoint costs one
+// GF(2) jump (a ~10k-tap correlation over 20k words in LDS).  Aim at a few
+// hundred segments for the words the job needs: enough workgroups to fill
+// the chip, few enough that the jumps stay cheap (measured with
+// tools/sim_ranks.py on config 4: 1024 for a 4K frame, 256-512 for a
+// 1/8-frame rank; small frames get short segments).  RT_JITTER_K overrides
+// (diagnostics).
+int jitter_k(int64_t words_needed) {
     static const int env_k = [] {
         const char* e = std::getenv("RT_JITTER_K");
         return e ? std::atoi(e) : 0;
     }();
     if (env_k > 0) return env_k;
-    // measured on config 4 (tools/sim_ranks.py): 1024 wins for whole frames,
-    // 512 from half a frame down (8 ranks: 0.62 -> 0.53 ms)
-    return words_needed * 4 > q_max * 3 ? kJitterK : kJitterKSmall;
+    int K = kJitterKMax;
+    while (K > kJitterKMin && words_needed / (624 * 128) < K) K >>= 1;
+    return K;
 }
 
 struct StdParams {
@@ -389,7 +392,7 @@ struct Workspace {
     DBuf nodes, mats, lights, objs, ops, gb;
     DBuf rows, jit, ckpt, jscratch, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
-    rtamd::JitterPlan jplan[2];   // K = kJitterK, kJitterKSmall (or the override)
+    std::map<int, rtamd::JitterPlan> jplan;   // per segment length K
     rtamd::JitterJob jjob;
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -569,8 +572,8 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
                 ws.jranges.push_back(rtamd::JRange{row_q * y, row_q * (y + 1), (int64_t)k * 16 * W});
         }
         const int64_t q1 = ws.jranges.back().qb;
-        const int K = jitter_k(row_q * n_rows, q1);
-        rtamd::JitterPlan& plan = ws.jplan[K == kJitterK ? 0 : 1];
+        const int K = jitter_k(row_q * n_rows);
+        rtamd::JitterPlan& plan = ws.jplan[K];
         const int levels = rtamd::mt_levels_needed(K, q1);
         if (plan.K != K || plan.levels < levels) {
             try {

@@ -51,7 +51,7 @@ def test_jitter_stream_matches_serial(gpu, q0, q1, first, count):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K", [256, 512])
+@pytest.mark.parametrize("K", [64, 256, 512])
 @pytest.mark.parametrize("q0,q1,first,count", [
     (0, 40 * SEG, 0, 2048),
     (FRAME_4K - 32 * 3840 * 8, FRAME_4K, FRAME_4K // 2 - 16 * 3840 * 8, 16 * 3840 * 8),   # last strip of 4K
