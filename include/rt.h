@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2   /* 2: rt_scene_desc gained directional lights */
 
 /* ---------------------------------------------------------------- errors */
 enum rt_status {
@@ -116,6 +116,15 @@ typedef struct rt_light {      /* scene.h:21-26 PointLight */
     double intensity[3];
 } rt_light;
 
+/* scene.h:10-15 DirectionalLight.  The JSON loader never creates one
+ * (json_loader.cpp has no key for it); they are reachable through
+ * rt_scene_from_desc, as the reference's Scene::dir_lights is through its API,
+ * and shaded before the point lights (shading.cpp:45-76). */
+typedef struct rt_dir_light {
+    double dir[3];             /* direction from the light toward the scene (incident) */
+    double radiance[3];
+} rt_dir_light;
+
 typedef struct rt_camera {     /* camera.h:7-79 Camera + ScreenSpec */
     double eye[3];
     double P[3];
@@ -139,6 +148,9 @@ typedef struct rt_scene_desc {
     int32_t n_objects;         /* top-level objects, in JSON order */
     int32_t pad_;
     const int32_t* objects;    /* node index of each top-level object */
+    int32_t n_dir_lights;      /* scene.h:36 dir_lights (ABI 2) */
+    int32_t pad2_;
+    const rt_dir_light* dir_lights;
 } rt_scene_desc;
 
 /* ScreenSpec::nx/ny (camera.h:19-21): max(1, int(round(L * dpi))). */

@@ -465,8 +465,8 @@ static inline V3 combine(V3 a, V3 b) {
     return v3(1.0 - (1.0 - a.x) * (1.0 - b.x), 1.0 - (1.0 - a.y) * (1.0 - b.y), 1.0 - (1.0 - a.z) * (1.0 - b.z));
 }
 
-/* shade_lambert_phong (shading.cpp:31-138); directional lights are never
- * populated by the loader and are omitted. */
+/* shade_lambert_phong (shading.cpp:31-138): directional lights (:45-76,
+ * reachable through rt_scene_from_desc only) then point lights (:79-130). */
 static V3 shade(Ctx* c, const Hit* hit, V3 wo) {
     if (hit->mat < 0) return v3(1, 0, 1);
     const rt_scene_desc* s = c->s;
@@ -475,6 +475,31 @@ static V3 shade(Ctx* c, const Hit* hit, V3 wo) {
     const V3 n = hit->n;
     V3 E_total = v3(m->ambient[0] * s->ambient[0], m->ambient[1] * s->ambient[1], m->ambient[2] * s->ambient[2]);
     const double shadow_epsilon = dmax(1e-3, 1e-4 * hit->t);
+    for (int li = 0; li < s->n_dir_lights; ++li) {
+        const rt_dir_light* L = &s->dir_lights[li];
+        c->st.ops[RT_OPC_LIGHT_EVAL]++;
+        V3 wi = normalized(v3(-L->dir[0], -L->dir[1], -L->dir[2]));   /* (-light.dir).normalized() */
+        double ndotl = dmax(0.0, dot3(n, wi));
+        if (ndotl <= 0.0) continue;
+        V3 so = v3(hit->p.x + n.x * shadow_epsilon, hit->p.y + n.y * shadow_epsilon, hit->p.z + n.z * shadow_epsilon);
+        Ray sr = make_ray(so, wi);
+        if (scene_occluded(c, &sr, shadow_epsilon, INFINITY)) continue;
+        c->st.ops[RT_OPC_SHADE_LIGHT]++;
+        /* scale(mul(albedo, radiance), kd * ndotl) */
+        double sd = m->kd * ndotl;
+        V3 E_d = v3(m->albedo[0] * L->radiance[0] * sd, m->albedo[1] * L->radiance[1] * sd,
+                    m->albedo[2] * L->radiance[2] * sd);
+        V3 E_s = v3(0, 0, 0);
+        if (m->ks > 0.0) {
+            c->st.ops[RT_OPC_SHADE_SPEC]++;
+            V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
+                                  2.0 * dot3(n, wi) * n.z - wi.z));
+            double rdotv = dmax(0.0, dot3(rr, wo));
+            double spec = pow(rdotv, m->shininess) * m->ks;
+            E_s = v3(L->radiance[0] * spec, L->radiance[1] * spec, L->radiance[2] * spec);
+        }
+        E_total = combine(E_total, combine(E_d, E_s));
+    }
     for (int li = 0; li < s->n_lights; ++li) {
         const rt_light* L = &s->lights[li];
         c->st.ops[RT_OPC_LIGHT_EVAL]++;

@@ -125,6 +125,12 @@ std::unique_ptr<Built> build(const rt_scene_desc* d) {
         L.intensity = Color(d->lights[i].intensity[0], d->lights[i].intensity[1], d->lights[i].intensity[2]);
         b->scene.point_lights.push_back(L);
     }
+    for (int i = 0; i < d->n_dir_lights; ++i) {
+        DirectionalLight L;
+        L.dir = Dir3(d->dir_lights[i].dir[0], d->dir_lights[i].dir[1], d->dir_lights[i].dir[2]);
+        L.radiance = Color(d->dir_lights[i].radiance[0], d->dir_lights[i].radiance[1], d->dir_lights[i].radiance[2]);
+        b->scene.dir_lights.push_back(L);
+    }
     b->scene.background = Color(d->background[0], d->background[1], d->background[2]);
     b->scene.ambient = Color(d->ambient[0], d->ambient[1], d->ambient[2]);
     b->scene.medium_index = d->medium_index;

@@ -104,10 +104,12 @@ struct DevScene {
     const rt_node* nodes;
     const rt_material* mats;
     const rt_light* lights;
+    const rt_dir_light* dlights;
     const DevObj* objs;
     const DevOp* ops;
     const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
     int n_lights, n_objs;
+    int n_dlights;
     int cam_nx, cam_ny;
     int rec_limit, cull;
     double eye[3], P[3], Lx, Ly;
@@ -1112,7 +1114,9 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 
 // shade_lambert_phong (shading.cpp:31-138), point lights only (the loader
 // never populates directional lights).
-template <bool EAGER, bool DEEP, class CT>
+// DL: the scene may have directional lights (the lean kernels, chosen only
+// for scenes without, do not carry their code or registers).
+template <bool EAGER, bool DEEP, bool DL, class CT>
 __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
     if (hit.mat < 0) return v3(1.0, 0.0, 1.0);
     cnt.inc(RT_OPC_SHADE_CALL);
@@ -1128,6 +1132,32 @@ __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32
     {
         const rt_material* m = &S.mats[hit.mat];
         E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
+    }
+    // directional lights first (shading.cpp:45-76): no falloff, shadow ray to infinity
+    for (int li = 0; DL && li < S.n_dlights; ++li) {
+        const rt_dir_light* L = &S.dlights[li];
+        cnt.inc(RT_OPC_LIGHT_EVAL);
+        const V3 wi = normalized(v3(-L->dir[0], -L->dir[1], -L->dir[2]));
+        const double ndotl = dmax(0.0, dot3(n, wi));
+        if (ndotl <= 0.0) continue;
+        const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
+        ++n_occl;
+        if (scene_occluded<EAGER, DEEP>(S, make_ray(so, wi), eps, RT_INF, cnt)) continue;
+        cnt.inc(RT_OPC_SHADE_LIGHT);
+        const rt_material* m = &S.mats[hit.mat];
+        const double sd = m->kd * ndotl;   // scale(mul(albedo, radiance), kd * ndotl)
+        const V3 Ed = v3(m->albedo[0] * L->radiance[0] * sd, m->albedo[1] * L->radiance[1] * sd,
+                         m->albedo[2] * L->radiance[2] * sd);
+        V3 Es = v3(0.0, 0.0, 0.0);
+        if (m->ks > 0.0) {
+            cnt.inc(RT_OPC_SHADE_SPEC);
+            const V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
+                                        2.0 * dot3(n, wi) * n.z - wi.z));
+            const double rdotv = dmax(0.0, dot3(rr, wo));
+            const double spec = pow(rdotv, m->shininess) * m->ks;
+            Es = v3(L->radiance[0] * spec, L->radiance[1] * spec, L->radiance[2] * spec);
+        }
+        E = combine(E, combine(Ed, Es));
     }
     for (int l0 = 0; l0 < S.n_lights; l0 += 32) {
         const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
@@ -1198,7 +1228,7 @@ struct Frame {
 };
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
-template <bool EAGER, bool DEEP, bool SECONDARY, class CT>
+template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, class CT>
 __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     if constexpr (!SECONDARY) {
         // No material reflects or refracts (or recursion <= 1): trace_recursive
@@ -1208,7 +1238,7 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         DHit h;
         ++n_isect;
         if (!scene_intersect<EAGER, DEEP>(S, r, 1e-4, RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
-        return shade<EAGER, DEEP>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
+        return shade<EAGER, DEEP, DL>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
     }
     Frame stk[kMaxDepth];
     int sp = 0;
@@ -1228,7 +1258,7 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
                 ret = v3(S.bg[0], S.bg[1], S.bg[2]);
             } else {
                 const V3 wo = normalized(vneg(r.d));
-                const V3 direct = shade<EAGER, DEEP>(S, ht, h, wo, n_occl, cnt);
+                const V3 direct = shade<EAGER, DEEP, DL>(S, ht, h, wo, n_occl, cnt);
                 if (h.mat < 0) {
                     ret = direct;
                 } else {

@@ -107,7 +107,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #define RT_LEAN_WAVES 4
 #endif
 
-template <bool E, bool D, bool SEC, bool C>
+template <bool E, bool D, bool SEC, bool C, bool DL = true>
 __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -125,7 +125,7 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
         // draws 16p+2s, 16p+2s+1 of the stream: dx, dy (tracer.cpp:293)
         const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)P.jrow[ri] * P.W + x) * 16 + 2 * s);
         const DRay ray = gen_ray_subpixel(S, x, y, j.x, j.y);
-        c = trace<E, D, SEC>(S, ray, ni, no, cnt);
+        c = trace<E, D, SEC, DL>(S, ray, ni, no, cnt);
     }
     // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
     const int base = lane & ~7;
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
 template <bool C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
                                                                                                        StdParams P) {
-    std_body<false, false, false, C>(S, P);
+    std_body<false, false, false, C, false>(S, P);
 }
 
 struct PaperParams {
@@ -181,7 +181,7 @@ struct PaperParams {
     unsigned long long* counters;
 };
 
-template <bool E, bool D, bool C>
+template <bool E, bool D, bool C, bool DL = true>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
@@ -209,7 +209,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         if (P.ext_shade[ei]) {
             // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
             V3 base = v3(1.0, 1.0, 1.0);
-            if (hits) base = shade<E, D>(S, ht, h, normalized(vneg(r.d)), no, cnt);
+            if (hits) base = shade<E, D, DL>(S, ht, h, normalized(vneg(r.d)), no, cnt);
             P.lum[idx] = 0.299 * base.x + 0.587 * base.y + 0.114 * base.z;
         }
     }
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
 template <bool C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
-    paper_primary_body<false, false, C>(S, P);
+    paper_primary_body<false, false, C, false>(S, P);
 }
 
 // apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
@@ -389,7 +389,7 @@ struct DBuf {
 // Per-device workspace (one render at a time per device; guarded by a mutex).
 struct Workspace {
     std::mutex mu;
-    DBuf nodes, mats, lights, objs, ops, gb;
+    DBuf nodes, mats, lights, dlights, objs, ops, gb;
     DBuf rows, jit, ckpt, jscratch, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
     std::map<int, rtamd::JitterPlan> jplan;   // per segment length K
@@ -446,6 +446,7 @@ struct rt_frame {
     std::vector<rt_node> nodes;
     std::vector<rt_material> mats;
     std::vector<rt_light> lights;
+    std::vector<rt_dir_light> dlights;
 };
 
 namespace {
@@ -503,7 +504,9 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->mode = mode;
     f->n_rows = n_rows;
     f->eager = cs.has_eager;
-    f->deep = cs.max_ivl_depth > 2;
+    // the lean kernels carry no directional-light code: such scenes take the
+    // general (D) variants
+    f->deep = cs.max_ivl_depth > 2 || d.n_dir_lights > 0;
     f->secondary = secondary;
     f->count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
     f->rows.assign(rows_host, rows_host + n_rows);
@@ -515,10 +518,12 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->nodes.assign(d.nodes, d.nodes + d.n_nodes);
     f->mats.assign(d.materials, d.materials + d.n_materials);
     f->lights.assign(d.lights, d.lights + d.n_lights);
+    f->dlights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
     f->cs = std::move(cs);
     HIP_TRY(upload(ws.nodes, f->nodes, st));
     HIP_TRY(upload(ws.mats, f->mats, st));
     HIP_TRY(upload(ws.lights, f->lights, st));
+    HIP_TRY(upload(ws.dlights, f->dlights, st));
     HIP_TRY(upload(ws.objs, f->cs.objs, st));
     HIP_TRY(upload(ws.ops, f->cs.ops, st));
     HIP_TRY(upload(ws.gb, f->cs.gbounds, st));
@@ -530,6 +535,8 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.nodes = ws.nodes.as<rt_node>();
     S.mats = ws.mats.as<rt_material>();
     S.lights = ws.lights.as<rt_light>();
+    S.dlights = ws.dlights.as<rt_dir_light>();
+    S.n_dlights = d.n_dir_lights;
     S.objs = ws.objs.as<DevObj>();
     S.ops = ws.ops.as<DevOp>();
     S.gb = ws.gb.as<float>();

@@ -95,9 +95,10 @@ namespace rtamd {
 
 bool validate_desc(const rt_scene_desc& d, std::string* why) {
     auto bad = [&](const std::string& m) { if (why) *why = m; return false; };
-    if (d.n_lights < 0 || d.n_materials < 0 || d.n_nodes < 0 || d.n_objects < 0) return bad("negative count");
+    if (d.n_lights < 0 || d.n_materials < 0 || d.n_nodes < 0 || d.n_objects < 0 || d.n_dir_lights < 0)
+        return bad("negative count");
     if ((d.n_lights && !d.lights) || (d.n_materials && !d.materials) || (d.n_nodes && !d.nodes) ||
-        (d.n_objects && !d.objects))
+        (d.n_objects && !d.objects) || (d.n_dir_lights && !d.dir_lights))
         return bad("NULL array with non-zero count");
     for (int i = 0; i < d.n_objects; ++i)
         if (d.objects[i] < 0 || d.objects[i] >= d.n_nodes) return bad("object index out of range");

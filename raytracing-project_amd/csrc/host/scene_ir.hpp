@@ -27,6 +27,7 @@ struct SceneIR {
     double medium_index = 1.0;
     int recursion_limit = 5;
     std::vector<rt_light> lights;
+    std::vector<rt_dir_light> dir_lights;
     std::vector<rt_material> materials;
     std::vector<rt_node> nodes;
     std::vector<int32_t> objects;

@@ -141,6 +141,8 @@ rt_scene_desc SceneIR::desc() const {
     d.nodes = nodes.empty() ? nullptr : nodes.data();
     d.n_objects = (int32_t)objects.size();
     d.objects = objects.empty() ? nullptr : objects.data();
+    d.n_dir_lights = (int32_t)dir_lights.size();
+    d.dir_lights = dir_lights.empty() ? nullptr : dir_lights.data();
     return d;
 }
 
@@ -154,6 +156,7 @@ SceneIR SceneIR::from_desc(const rt_scene_desc& d) {
     if (d.n_materials > 0) s.materials.assign(d.materials, d.materials + d.n_materials);
     if (d.n_nodes > 0) s.nodes.assign(d.nodes, d.nodes + d.n_nodes);
     if (d.n_objects > 0) s.objects.assign(d.objects, d.objects + d.n_objects);
+    if (d.n_dir_lights > 0) s.dir_lights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
     return s;
 }
 

@@ -64,6 +64,10 @@ class Light(C.Structure):
     _fields_ = [("pos", C.c_double * 3), ("intensity", C.c_double * 3)]
 
 
+class DirLight(C.Structure):
+    _fields_ = [("dir", C.c_double * 3), ("radiance", C.c_double * 3)]
+
+
 class Camera(C.Structure):
     _fields_ = [("eye", C.c_double * 3), ("P", C.c_double * 3), ("Lx", C.c_double), ("Ly", C.c_double),
                 ("dpi", C.c_int32), ("pad_", C.c_int32)]
@@ -74,7 +78,8 @@ class SceneDesc(C.Structure):
                 ("medium_index", C.c_double), ("recursion_limit", C.c_int32), ("n_lights", C.c_int32),
                 ("lights", C.POINTER(Light)), ("n_materials", C.c_int32), ("n_nodes", C.c_int32),
                 ("materials", C.POINTER(Material)), ("nodes", C.POINTER(Node)), ("n_objects", C.c_int32),
-                ("pad_", C.c_int32), ("objects", C.POINTER(C.c_int32))]
+                ("pad_", C.c_int32), ("objects", C.POINTER(C.c_int32)), ("n_dir_lights", C.c_int32),
+                ("pad2_", C.c_int32), ("dir_lights", C.POINTER(DirLight))]
 
 
 class Stats(C.Structure):
@@ -272,6 +277,21 @@ def scene_from_desc(desc: SceneDesc) -> Scene:
     if rc != RT_OK:
         raise RTError(rc, last_error())
     return Scene(out.value)
+
+
+def with_dir_lights(scene: Scene, lights) -> Scene:
+    """Copy of `scene` with directional lights [(dir, radiance), ...]: the
+    reference's Scene::dir_lights (scene.h:10-15, 36), which its JSON loader
+    never fills; reachable here through rt_scene_from_desc as there through
+    the Scene API."""
+    d = SceneDesc.from_buffer_copy(scene.desc)   # arrays are deep-copied by rt_scene_from_desc
+    arr = (DirLight * max(1, len(lights)))()
+    for i, (dv, rad) in enumerate(lights):
+        arr[i].dir[:] = [float(v) for v in dv]
+        arr[i].radiance[:] = [float(v) for v in rad]
+    d.n_dir_lights = len(lights)
+    d.dir_lights = C.cast(arr, C.POINTER(DirLight))
+    return scene_from_desc(d)
 
 
 def device_count() -> int:

@@ -292,3 +292,22 @@ def torture_scenes(dpi: int = 24) -> dict[str, dict]:
         ],
     }
     return sc
+
+
+def dir_light_cases(dpi: int = 16) -> dict[str, tuple[str, list]]:
+    """Scenes with directional lights (the reference's Scene::dir_lights,
+    scene.h:10-15; its loader never creates them, so they are attached to the
+    IR: rtamd.with_dir_lights).  Cases: a sun and a back light beside point
+    lights, a zero direction (Vec4::normalized's (0,1,0) fallback,
+    core.h:58-64), the deep-CSG scene, and reflection/refraction recursion."""
+    sun = ([-0.4, -1.0, -0.3], [0.9, 0.85, 0.8])
+    back = ([0.0, 0.3, 1.0], [0.3, 0.3, 0.5])       # from behind the camera's view: mostly ndotl <= 0
+    zero = ([0.0, 0.0, 0.0], [0.2, 0.2, 0.2])
+    tort = torture_scenes(dpi=dpi)
+    return {
+        "cfg2_sun_back": (config_json(2, dpi=dpi)[0], [sun, back]),
+        "cfg2_zero_dir": (config_json(2, dpi=dpi)[0], [zero]),
+        "snorlax_sun": (json.dumps(with_dpi(load_example("snorlax"), dpi)), [sun]),
+        "reflect_refract_sun": (json.dumps(tort["reflect_refract"]), [sun, back]),
+        "pokeball_csg_sun": (json.dumps(tort["pokeball_csg"]), [sun]),
+    }

@@ -13,6 +13,10 @@ turned into IR by our loader (librt_host.so).  Outputs are data only:
   jitter.npz   draws of std::mt19937(12345) + uniform_real_distribution(-0.5,0.5)
                at pixel/sample offsets up to the last pixels of 8K
   cameras.npz  Camera::generate_ray / generate_ray_subpixel outputs
+  dirlights.npz  frames + counts of scenes with directional lights attached
+               (scenes.dir_light_cases), standard and paper mode
+
+Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights]
 """
 from __future__ import annotations
 
@@ -165,8 +169,28 @@ def make_cameras():
     print("cameras:", len(data))
 
 
+def make_dirlights():
+    """Directional-light frames (scenes.dir_light_cases), both modes."""
+    data = {}
+    for name, (text, lights) in scenes.dir_light_cases().items():
+        sc = rtamd.with_dir_lights(rtamd.load_scene_from_json_text(text), lights)
+        for mode in (0, 1):
+            with quiet_stdout():
+                fb, ni, no = rtamd.ref_render(sc, sc.width, sc.height, mode)
+            data[f"{name}/{mode}/fb"] = fb
+            data[f"{name}/{mode}/counts"] = np.array([ni, no], dtype=np.int64)
+        data[f"{name}/lights"] = np.array(lights, dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "dirlights.npz"), **data)
+    print("dirlights:", len(data))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for what in sys.argv[1:]:
+            globals()["make_" + what]()
+        sys.exit(0)
     make_frames()
     make_kats()
     make_jitter()
     make_cameras()
+    make_dirlights()

@@ -82,3 +82,21 @@ def test_opcounts_match_reference_without_cull(gpu, name):
     o = {n: int(ost.ops[i]) for i, n in enumerate(rt.OP_NAMES)}
     assert {n: g[n] for n in FLOP_COUNTERS} == {n: o[n] for n in FLOP_COUNTERS}
     assert (st.rays_intersect, st.rays_occluded) == (ost.rays_intersect, ost.rays_occluded)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dir_lights_match_oracle(gpu, mode):
+    """Scenes with directional lights attached through the IR (the reference's
+    loader never creates them) on the general kernels."""
+    rt = gpu
+    for name, (text, lights) in scenes.dir_light_cases().items():
+        sc = rt.with_dir_lights(rt.load_scene_from_json_text(text), lights)
+        W, H = sc.width, sc.height
+        st = rt.Stats()
+        fb = rt.Tracer(sc, W, H, mode).render(st)
+        ref, ost = rt.oracle_render(sc, W, H, mode, threads=8)
+        assert float(np.abs(fb - ref).max()) <= TOL, name
+        if mode == 1:
+            assert np.array_equal(fb, ref), name
+        assert (st.rays_intersect, st.rays_occluded) == (ost.rays_intersect, ost.rays_occluded), name

@@ -32,7 +32,7 @@ def test_libraries_export_every_declared_symbol():
     assert len(declared) >= 18 and "rt_render" in declared and "rt_last_error" in declared
     for name in declared:
         assert hasattr(host, name) or hasattr(amd, name), name
-    assert amd.rt_abi_version() == 1
+    assert amd.rt_abi_version() == 2
 
 
 def _decode_png(path):

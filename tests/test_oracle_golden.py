@@ -251,3 +251,20 @@ def test_full_resolution_checksums(rt, name, mode, checksum, ni, no):
         s += v[0] + v[1] + v[2]
     assert s == checksum
     assert (st.rays_intersect, st.rays_occluded) == (ni, no)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_oracle_dir_lights_bit_exact(rt, mode):
+    """Directional lights (shading.cpp:45-76) against frames of the reference
+    itself (tests/golden/dirlights.npz, made from oracle/_ref)."""
+    import scenes
+
+    gold = np.load(os.path.join(GOLDEN, "dirlights.npz"))
+    for name, (text, lights) in scenes.dir_light_cases().items():
+        assert np.array_equal(np.array(lights, dtype=np.float64), gold[f"{name}/lights"]), name
+        sc = rt.with_dir_lights(rt.load_scene_from_json_text(text), lights)
+        assert sc.desc.n_dir_lights == len(lights)
+        fb, st = rt.oracle_render(sc, sc.width, sc.height, mode, threads=4)
+        assert np.array_equal(fb, gold[f"{name}/{mode}/fb"]), name
+        cnt = gold[f"{name}/{mode}/counts"]
+        assert (st.rays_intersect, st.rays_occluded) == (int(cnt[0]), int(cnt[1])), name
