@@ -57,6 +57,9 @@ def main() -> int:
     ap.add_argument("--cpu-rows", type=int, default=64, help="rows in the CPU-oracle baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cull", action="store_true", help="disable wave-uniform bound culling")
+    ap.add_argument("--fp32", action="store_true",
+                    help="time the NON-PARITY FP32 fast path as the headline (RT_FLAG_FP32); default is FP64")
+    ap.add_argument("--fp32-steps", type=int, default=3, help="frames of the FP32 side leg (0 = skip)")
     ap.add_argument("--chunks", type=int, default=4, help="row chunks per rank pipelined with the gather (N > 1)")
     args = ap.parse_args()
 
@@ -83,6 +86,8 @@ def main() -> int:
     W, H = sc.width, sc.height
     lib = rtamd.amd_lib()
     flags = rtamd.RT_FLAG_NO_CULL if args.no_cull else rtamd.RT_FLAG_NONE
+    if args.fp32:
+        flags |= rtamd.RT_FLAG_FP32
     dev = torch.device("cuda", local)
 
     df = frame_dist.DistFrame(W, H, rank, world, dev, chunks=args.chunks)
@@ -162,6 +167,38 @@ def main() -> int:
     step(flags | rtamd.RT_FLAG_COUNT_OPS, st_exe)
     torch.cuda.synchronize()
 
+    # Side leg (outside the timed region, not the headline): the NON-PARITY
+    # FP32 fast path (RT_FLAG_FP32) on the same frame.
+    fp32 = None
+    if args.fp32_steps > 0 and not args.fp32:
+        st32 = rtamd.Stats()
+        f32 = flags | rtamd.RT_FLAG_FP32
+        step(f32, st32)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t32 = time.perf_counter()
+        rays32, k32 = 0, []
+        for _ in range(args.fp32_steps):
+            step(f32, st32)
+            rays32 += st32.rays_intersect + st32.rays_occluded
+            k32.append(st32.ms_kernel)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        e32 = time.perf_counter() - t32
+        if dist:
+            t = torch.tensor([e32, rays32], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e32 = float(t[0].item())
+            r = torch.tensor([rays32], dtype=torch.float64, device=dev)
+            dist.all_reduce(r, op=dist.ReduceOp.SUM)
+            rays32 = float(r.item())
+        fp32 = {"value": round(rays32 / e32 / 1e6, 3), "unit": "Mrays/s",
+                "ms_per_step": round(e32 / args.fp32_steps * 1e3, 3),
+                "kernel_ms": round(sum(k32) / len(k32), 3), "steps": args.fp32_steps,
+                "note": "RT_FLAG_FP32: non-parity fast path, not within the 1e-5 tolerance (tests/test_gpu_fp32.py)"}
+
     if rank != 0:
         if dist:
             dist.barrier()
@@ -218,7 +255,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f32" if args.fp32 else "f64",
         "data": "synthetic: reference example scene JSON + mt19937(12345) jitter, rendered on device",
         "config": {"workload": name, "width": W, "height": H, "mode": "paper" if mode else "standard",
                    "rays_per_frame": int(rays_per_frame), "parallelism": f"row-strips{STRIP}x{world}" + (f", gather-to-rank0 in {len(df.bounds)} chunks" if world > 1 else ""),
@@ -235,6 +272,7 @@ def main() -> int:
                      round(prof_traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
         "rng_ms": round(sum(rng_ms) / len(rng_ms), 3),
         "cpu_baseline": cpu,
+        "fp32_fast_path": fp32,
     }
     print(json.dumps(out), flush=True)
     if dist:

@@ -7,6 +7,7 @@
 // Extra options may follow argv[3] (the reference ignores them):
 //   --stats        print one JSON line with ray counts and timings
 //   --threads N    deflate threads for the PNG writer (default 8)
+//   --fp32         NON-PARITY FP32 fast path (RT_FLAG_FP32)
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -29,8 +30,10 @@ int main(int argc, char** argv) {
     if (argc > 3 && std::string(argv[3]) == "--paper") paper_mode = true;
     bool print_stats = false;
     int png_threads = 8;
+    bool fp32 = false;
     for (int i = 3; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--stats")) print_stats = true;
+        else if (!std::strcmp(argv[i], "--fp32")) fp32 = true;
         else if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) png_threads = std::atoi(argv[++i]);
     }
 
@@ -54,6 +57,7 @@ int main(int argc, char** argv) {
     tracer.width = W;
     tracer.height = H;
     tracer.mode = paper_mode ? rtamd::RenderMode::Paper : rtamd::RenderMode::Standard;
+    if (fp32) tracer.flags |= RT_FLAG_FP32;
 
     if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";

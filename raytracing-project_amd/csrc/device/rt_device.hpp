@@ -13,40 +13,61 @@
 //   * transforms / CSG operands live on a ray stack and an interval stack
 //     whose top two intervals stay in VGPRs (left-deep folds never spill),
 //   * reflection / refraction recursion is an explicit per-lane frame stack.
-#pragma once
-
+//
+// Precision: the file is compiled once per arithmetic type.  RT_REAL double
+// (namespace rtd) is the parity path; RT_REAL float (namespace rtf,
+// rt_render_f32.hip, RT_FLAG_FP32) is the optional non-parity fast path of
+// the same algorithm on float scene copies.  Literals
+// go through RV() so the float build does no double arithmetic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "rt.h"
+#include "rt_launch.hpp"
 #include "scene_compile.hpp"
 
-namespace rtd {
+#ifndef RT_REAL
+#define RT_REAL double
+#define RT_NS rtd
+#endif
+
+namespace RT_NS {
 
 using rtamd::DevObj;
 using rtamd::DevOp;
+using real = RT_REAL;
+using NodeT = rtamd::NodeR<real>;
+using MatT = rtamd::MatR<real>;
+using LightT = rtamd::LightR<real>;
+using DLightT = rtamd::DLightR<real>;
+#define RV(x) static_cast<real>(x)
+#define RT_INF static_cast<real>(__builtin_inf())
 
-constexpr double kEPS = 1e-6;   // core.h:10
-#define RT_INF __builtin_inf()
+__device__ __forceinline__ double sqrt_r(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ double fabs_r(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float sqrt_r(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float fabs_r(float x) { return __builtin_fabsf(x); }
 
-constexpr int kMaxRayStack = 8;   // transform nesting (checked on the host)
-constexpr int kMaxIvlSpill = 6;   // interval stack entries beyond the top two
-constexpr int kMaxDepth = 16;     // recursion frames (medium.recursion <= 16)
+constexpr real kEPS = RV(1e-6);   // core.h:10
+
+using rtamd::kMaxDepth;
+using rtamd::kMaxIvlSpill;
+using rtamd::kMaxRayStack;
 
 struct V3 {
-    double x, y, z;
+    real x, y, z;
 };
-__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-__device__ __forceinline__ double dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ double dmax(double a, double b) { return (a < b) ? b : a; }   // std::max
-__device__ __forceinline__ double dmin(double a, double b) { return (b < a) ? b : a; }   // std::min
+__device__ __forceinline__ V3 v3(real x, real y, real z) { return V3{x, y, z}; }
+__device__ __forceinline__ real dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ real dmax(real a, real b) { return (a < b) ? b : a; }   // std::max
+__device__ __forceinline__ real dmin(real a, real b) { return (b < a) ? b : a; }   // std::min
 __device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
 
 // Dir3::normalized (core.h:95-101)
 __device__ __forceinline__ V3 normalized(V3 v) {
-    double L = __builtin_sqrt(dot3(v, v));
+    real L = sqrt_r(dot3(v, v));
     if (L > kEPS) return v3(v.x / L, v.y / L, v.z / L);
-    return v3(0.0, 1.0, 0.0);
+    return v3(RV(0.0), RV(1.0), RV(0.0));
 }
 
 struct DRay {
@@ -54,7 +75,7 @@ struct DRay {
 };
 // Ray::Ray (core.h:278) normalises the direction.
 __device__ __forceinline__ DRay make_ray(V3 o, V3 d) { return DRay{o, normalized(d)}; }
-__device__ __forceinline__ V3 ray_at(const DRay& r, double t) {   // core.h:280
+__device__ __forceinline__ V3 ray_at(const DRay& r, real t) {   // core.h:280
     return v3(r.o.x + r.d.x * t, r.o.y + r.d.y * t, r.o.z + r.d.z * t);
 }
 
@@ -67,19 +88,19 @@ struct DHit {
 
 // Hit::set_face_normal (geometry.h:42-45)
 __device__ __forceinline__ void set_face_normal(DHit& h, const DRay& r, V3 outward) {
-    h.ff = dot3(r.d, outward) < 0.0;
+    h.ff = dot3(r.d, outward) < RV(0.0);
     h.n = h.ff ? outward : vneg(outward);
 }
 
 struct Ivl {
     int ok;
-    double t0, t1;
+    real t0, t1;
     DHit h0, h1;
 };
 
 struct THit {   // intersect-mode hit
     int ok;
-    double t;
+    real t;
     DHit h;
 };
 
@@ -101,10 +122,10 @@ struct Cnt<true> {
 };
 
 struct DevScene {
-    const rt_node* nodes;
-    const rt_material* mats;
-    const rt_light* lights;
-    const rt_dir_light* dlights;
+    const NodeT* nodes;
+    const MatT* mats;
+    const LightT* lights;
+    const DLightT* dlights;
     const DevObj* objs;
     const DevOp* ops;
     const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
@@ -112,27 +133,27 @@ struct DevScene {
     int n_dlights;
     int cam_nx, cam_ny;
     int rec_limit, cull;
-    double eye[3], P[3], Lx, Ly;
-    double bg[3], amb[3], medium_index;
+    real eye[3], P[3], Lx, Ly;
+    real bg[3], amb[3], medium_index;
 };
 
-__device__ __forceinline__ V3 ld3(const double* p) { return v3(p[0], p[1], p[2]); }
+__device__ __forceinline__ V3 ld3(const real* p) { return v3(p[0], p[1], p[2]); }
 
 // --------------------------------------------------------------- primitives
 // Sphere::intersect (geometry.cpp:12-37)
 template <class CT>
-__device__ __forceinline__ bool sphere_intersect(V3 c, double rad, const DRay& ray, double tmin, double tmax,
-                                                 double& t_out, DHit& out, CT& cnt) {
+__device__ __forceinline__ bool sphere_intersect(V3 c, real rad, const DRay& ray, real tmin, real tmax,
+                                                 real& t_out, DHit& out, CT& cnt) {
     cnt.inc(RT_OPC_SPHERE_ISECT);
     V3 oc = v3(ray.o.x - c.x, ray.o.y - c.y, ray.o.z - c.z);
-    double half_b = dot3(oc, ray.d);
-    double cterm = dot3(oc, oc) - rad * rad;
-    double disc = half_b * half_b - 1.0 * cterm;
-    if (disc < 0.0) return false;
-    double sq = __builtin_sqrt(disc);
-    double t = (-half_b - sq) / 1.0;
+    real half_b = dot3(oc, ray.d);
+    real cterm = dot3(oc, oc) - rad * rad;
+    real disc = half_b * half_b - RV(1.0) * cterm;
+    if (disc < RV(0.0)) return false;
+    real sq = sqrt_r(disc);
+    real t = (-half_b - sq) / RV(1.0);
     if (t < tmin || t > tmax) {
-        t = (-half_b + sq) / 1.0;
+        t = (-half_b + sq) / RV(1.0);
         if (t < tmin || t > tmax) return false;
     }
     cnt.inc(RT_OPC_SPHERE_ISECT_HIT);
@@ -145,20 +166,20 @@ __device__ __forceinline__ bool sphere_intersect(V3 c, double rad, const DRay& r
 
 // Sphere::interval (geometry.cpp:48-78)
 template <class CT>
-__device__ __forceinline__ void sphere_interval(V3 c, double r, int mat, const DRay& ray, Ivl& o, CT& cnt) {
+__device__ __forceinline__ void sphere_interval(V3 c, real r, int mat, const DRay& ray, Ivl& o, CT& cnt) {
     cnt.inc(RT_OPC_SPHERE_IVL);
     V3 oc = v3(ray.o.x - c.x, ray.o.y - c.y, ray.o.z - c.z);
-    double half_b = dot3(oc, ray.d);
-    double cterm = dot3(oc, oc) - r * r;
-    double disc = half_b * half_b - 1.0 * cterm;
-    o.ok = !(disc < 0.0);
+    real half_b = dot3(oc, ray.d);
+    real cterm = dot3(oc, oc) - r * r;
+    real disc = half_b * half_b - RV(1.0) * cterm;
+    o.ok = !(disc < RV(0.0));
     if (!o.ok) return;
     cnt.inc(RT_OPC_SPHERE_IVL_HIT);
-    double s = __builtin_sqrt(disc);
-    double t0 = (-half_b - s) / 1.0;
-    double t1 = (-half_b + s) / 1.0;
+    real s = sqrt_r(disc);
+    real t0 = (-half_b - s) / RV(1.0);
+    real t1 = (-half_b + s) / RV(1.0);
     if (t0 > t1) {
-        double tt = t0;
+        real tt = t0;
         t0 = t1;
         t1 = tt;
     }
@@ -174,13 +195,13 @@ __device__ __forceinline__ void sphere_interval(V3 c, double r, int mat, const D
 
 // HalfSpace::intersect (geometry.cpp:90-106)
 template <class CT>
-__device__ __forceinline__ bool half_intersect(V3 p0, V3 n, const DRay& r, double tmin, double tmax, double& t_out,
+__device__ __forceinline__ bool half_intersect(V3 p0, V3 n, const DRay& r, real tmin, real tmax, real& t_out,
                                                DHit& out, CT& cnt) {
     cnt.inc(RT_OPC_HALF_ISECT);
-    const double ndotd = dot3(n, r.d);
-    if (__builtin_fabs(ndotd) < 1e-12) return false;
+    const real ndotd = dot3(n, r.d);
+    if (fabs_r(ndotd) < RV(1e-12)) return false;
     V3 diff = v3(p0.x - r.o.x, p0.y - r.o.y, p0.z - r.o.z);
-    const double t = dot3(n, diff) / ndotd;
+    const real t = dot3(n, diff) / ndotd;
     if (t < tmin || t > tmax) return false;
     cnt.inc(RT_OPC_HALF_ISECT_HIT);
     t_out = t;
@@ -193,21 +214,21 @@ __device__ __forceinline__ bool half_intersect(V3 p0, V3 n, const DRay& r, doubl
 template <class CT>
 __device__ __forceinline__ void half_interval(V3 p0, V3 n, int mat, const DRay& r, Ivl& o, CT& cnt) {
     cnt.inc(RT_OPC_HALF_IVL);
-    const double ndotd = dot3(n, r.d);
+    const real ndotd = dot3(n, r.d);
     V3 diff = v3(r.o.x - p0.x, r.o.y - p0.y, r.o.z - p0.z);
-    const double f0 = dot3(n, diff);
+    const real f0 = dot3(n, diff);
     o.h0.mat = mat;
     o.h1.mat = mat;
-    if (__builtin_fabs(ndotd) < 1e-12) {
-        o.ok = f0 >= 0.0;
+    if (fabs_r(ndotd) < RV(1e-12)) {
+        o.ok = f0 >= RV(0.0);
         o.t0 = -RT_INF;
         o.t1 = RT_INF;
         o.h0.p = r.o;
         o.h1.p = r.o;
     } else {
         o.ok = 1;
-        const double tPlane = -f0 / ndotd;
-        if (ndotd > 0.0) {
+        const real tPlane = -f0 / ndotd;
+        if (ndotd > RV(0.0)) {
             o.t0 = tPlane;
             o.t1 = RT_INF;
             o.h0.p = ray_at(r, tPlane);
@@ -223,30 +244,30 @@ __device__ __forceinline__ void half_interval(V3 p0, V3 n, int mat, const DRay& 
     set_face_normal(o.h1, r, n);
 }
 
-__device__ __forceinline__ double clamp1(double x) {   // geometry.cpp:152-156
-    if (x < -1.0) return -1.0;
-    if (x > 1.0) return 1.0;
+__device__ __forceinline__ real clamp1(real x) {   // geometry.cpp:152-156
+    if (x < -RV(1.0)) return -RV(1.0);
+    if (x > RV(1.0)) return RV(1.0);
     return x;
 }
 
 // Pokeball::pick_region_material (geometry.cpp:163-180)
 template <class CT>
-__device__ __forceinline__ int pick_region(const rt_node* nd, V3 p, CT& cnt) {
+__device__ __forceinline__ int pick_region(const NodeT* nd, V3 p, CT& cnt) {
     cnt.inc(RT_OPC_POKE_REGION);
-    const double* v = nd->v;
-    const double r = v[3];
+    const real* v = nd->v;
+    const real r = v[3];
     V3 u = v3((p.x - v[0]) / r, (p.y - v[1]) / r, (p.z - v[2]) / r);
-    const double ang = acos(clamp1(dot3(u, v3(v[7], v[8], v[9]))));
-    const double inner = dmax(0.0, v[5] - v[6]);
+    const real ang = acos(clamp1(dot3(u, v3(v[7], v[8], v[9]))));
+    const real inner = dmax(RV(0.0), v[5] - v[6]);
     if (ang <= v[5]) return (ang >= inner) ? nd->mats[RT_PB_RING] : nd->mats[RT_PB_BUTTON];
-    if (__builtin_fabs(u.y) <= v[4]) return nd->mats[RT_PB_BELT];
-    return (u.y >= 0.0) ? nd->mats[RT_PB_TOP] : nd->mats[RT_PB_BOTTOM];
+    if (fabs_r(u.y) <= v[4]) return nd->mats[RT_PB_BELT];
+    return (u.y >= RV(0.0)) ? nd->mats[RT_PB_TOP] : nd->mats[RT_PB_BOTTOM];
 }
 
 // Leaf Primitive::intersect for the three leaf kinds.
 template <class CT>
-__device__ __forceinline__ bool leaf_intersect(const rt_node* nd, const DRay& r, double tmin, double tmax,
-                                               double& t, DHit& h, CT& cnt) {
+__device__ __forceinline__ bool leaf_intersect(const NodeT* nd, const DRay& r, real tmin, real tmax,
+                                               real& t, DHit& h, CT& cnt) {
     const int kind = nd->kind;
     if (kind == RT_NODE_HALFSPACE) {
         bool ok = half_intersect(ld3(nd->v), ld3(nd->v + 3), r, tmin, tmax, t, h, cnt);
@@ -263,7 +284,7 @@ __device__ __forceinline__ bool leaf_intersect(const rt_node* nd, const DRay& r,
 }
 
 template <class CT>
-__device__ __forceinline__ void leaf_interval(const rt_node* nd, const DRay& r, Ivl& o, CT& cnt) {
+__device__ __forceinline__ void leaf_interval(const NodeT* nd, const DRay& r, Ivl& o, CT& cnt) {
     const int kind = nd->kind;
     if (kind == RT_NODE_HALFSPACE) {
         half_interval(ld3(nd->v), ld3(nd->v + 3), nd->mat, r, o, cnt);
@@ -278,46 +299,46 @@ __device__ __forceinline__ void leaf_interval(const rt_node* nd, const DRay& r, 
 
 // ---------------------------------------------------------------- transforms
 // Matrix4 * Vec4 rows 0..2 (core.h:169-176)
-__device__ __forceinline__ V3 mat_apply(const double* m, V3 v, double w) {
+__device__ __forceinline__ V3 mat_apply(const real* m, V3 v, real w) {
     return v3(m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3] * w, m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7] * w,
               m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11] * w);
 }
 
 // Local ray of Translation / Scaling / Rotation (transform.cpp:24-29, 97-111, 184-196).
 // Degenerate Scaling never reaches the device (compiled to OP_NEVER).
-__device__ __forceinline__ DRay local_ray(const rt_node* nd, const DRay& r) {
-    const double* M = nd->v;
+__device__ __forceinline__ DRay local_ray(const NodeT* nd, const DRay& r) {
+    const real* M = nd->v;
     const int kind = nd->kind;
     if (kind == RT_NODE_TRANSLATION) return make_ray(v3(r.o.x - M[3], r.o.y - M[7], r.o.z - M[11]), r.d);
     if (kind == RT_NODE_SCALING) {
-        const double sx = M[0], sy = M[5], sz = M[10];
+        const real sx = M[0], sy = M[5], sz = M[10];
         return make_ray(v3(r.o.x / sx, r.o.y / sy, r.o.z / sz), v3(r.d.x / sx, r.d.y / sy, r.d.z / sz));
     }
-    const double* I = nd->v + 12;
-    return make_ray(mat_apply(I, r.o, 1.0), mat_apply(I, r.d, 0.0));
+    const real* I = nd->v + 12;
+    return make_ray(mat_apply(I, r.o, RV(1.0)), mat_apply(I, r.d, RV(0.0)));
 }
 
-__device__ __forceinline__ V3 map_point(const rt_node* nd, V3 p) {
-    const double* M = nd->v;
+__device__ __forceinline__ V3 map_point(const NodeT* nd, V3 p) {
+    const real* M = nd->v;
     const int kind = nd->kind;
     if (kind == RT_NODE_TRANSLATION) return v3(p.x + M[3], p.y + M[7], p.z + M[11]);
     if (kind == RT_NODE_SCALING) return v3(p.x * M[0], p.y * M[5], p.z * M[10]);
-    return mat_apply(M, p, 1.0);
+    return mat_apply(M, p, RV(1.0));
 }
 
-__device__ __forceinline__ V3 map_normal(const rt_node* nd, V3 n) {
-    const double* M = nd->v;
+__device__ __forceinline__ V3 map_normal(const NodeT* nd, V3 n) {
+    const real* M = nd->v;
     const int kind = nd->kind;
     if (kind == RT_NODE_TRANSLATION) return n;
     if (kind == RT_NODE_SCALING) return normalized(v3(n.x / M[0], n.y / M[5], n.z / M[10]));
-    return normalized(mat_apply(M, n, 0.0));
+    return normalized(mat_apply(M, n, RV(0.0)));
 }
 
 // Transform::project_t_world (transform.h:76-80)
-__device__ __forceinline__ double project_t_world(const DRay& r, V3 Pw) {
+__device__ __forceinline__ real project_t_world(const DRay& r, V3 Pw) {
     V3 v = v3(Pw.x - r.o.x, Pw.y - r.o.y, Pw.z - r.o.z);
-    const double dd = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
-    return dd > 0.0 ? (v.x * r.d.x + v.y * r.d.y + v.z * r.d.z) / dd : RT_INF;
+    const real dd = r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z;
+    return dd > RV(0.0) ? (v.x * r.d.x + v.y * r.d.y + v.z * r.d.z) / dd : RT_INF;
 }
 
 // ------------------------------------------------------------------- CSG
@@ -326,8 +347,8 @@ __device__ __forceinline__ bool csg_combine(int op, bool a, bool b) {
 }
 
 // event_less lambda (csg.cpp:87-92); code = who*2 + type (type 0 Enter, 1 Exit)
-__device__ __forceinline__ bool ev_less(double ta, int ca, double tb, int cb) {
-    if (__builtin_fabs(ta - tb) > 1e-6) return ta < tb;
+__device__ __forceinline__ bool ev_less(real ta, int ca, real tb, int cb) {
+    if (fabs_r(ta - tb) > RV(1e-6)) return ta < tb;
     const int tya = ca & 1, tyb = cb & 1;
     if (tya != tyb) return tya == 0;
     return (ca >> 1) < (cb >> 1);
@@ -345,11 +366,11 @@ __device__ __forceinline__ void csg_interval(int op, const Ivl& A, const Ivl& B,
     if (!A.ok && !B.ok) return;
     cnt.inc(RT_OPC_CSG_COMBINE);
     // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
-    double et[4];
+    real et[4];
     int ec[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        et[k] = 0.0;
+        et[k] = RV(0.0);
         ec[k] = 0;
     }
     int n = 0;
@@ -358,7 +379,7 @@ __device__ __forceinline__ void csg_interval(int op, const Ivl& A, const Ivl& B,
         const bool p1 = A.ok && __builtin_isfinite(A.t1);
         const bool p2 = B.ok && __builtin_isfinite(B.t0);
         const bool p3 = B.ok && __builtin_isfinite(B.t1);
-        const double tv[4] = {A.t0, A.t1, B.t0, B.t1};
+        const real tv[4] = {A.t0, A.t1, B.t0, B.t1};
         const bool pv[4] = {p0, p1, p2, p3};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -376,7 +397,7 @@ __device__ __forceinline__ void csg_interval(int op, const Ivl& A, const Ivl& B,
 #pragma unroll
     for (int i = 1; i < 4; ++i) {
         if (i < n) {
-            const double vt = et[i];
+            const real vt = et[i];
             const int vc = ec[i];
             if (ev_less(vt, vc, et[0], ec[0])) {
 #pragma unroll
@@ -410,13 +431,13 @@ __device__ __forceinline__ void csg_interval(int op, const Ivl& A, const Ivl& B,
             }
         }
     }
-    bool inA = A.ok && (A.t0 < 1e-6) && (A.t1 > 1e-6);
-    bool inB = B.ok && (B.t0 < 1e-6) && (B.t1 > 1e-6);
+    bool inA = A.ok && (A.t0 < RV(1e-6)) && (A.t1 > RV(1e-6));
+    bool inB = B.ok && (B.t0 < RV(1e-6)) && (B.t1 > RV(1e-6));
     bool inR = csg_combine(op, inA, inB);
     bool haveEnter = false;
     int enterCode = -1, exitCode = -1;
     bool flipE = false, flipX = false;
-    double tEnt = 0.0, tExt = RT_INF;
+    real tEnt = RV(0.0), tExt = RT_INF;
     int originMat = -1;
     if (inR) {
         haveEnter = true;
@@ -452,7 +473,7 @@ __device__ __forceinline__ void csg_interval(int op, const Ivl& A, const Ivl& B,
     R.t1 = tExt;
     if (enterCode < 0) {
         R.h0.p = ray.o;
-        R.h0.n = v3(0.0, 0.0, 0.0);
+        R.h0.n = v3(RV(0.0), RV(0.0), RV(0.0));
         R.h0.mat = originMat;
         R.h0.ff = 1;
     } else {
@@ -485,8 +506,8 @@ struct IStack {
 
 // Evaluate one OBJ_PROG object: Primitive::intersect(root, ray, tmin, tmax).
 template <bool EAGER, class CT>
-__device__ __forceinline__ bool run_program(const DevScene& S, int pc0, int pc1, const DRay& world, double tmin,
-                                         double tmax, double& t_out, DHit& h_out, CT& cnt) {
+__device__ __forceinline__ bool run_program(const DevScene& S, int pc0, int pc1, const DRay& world, real tmin,
+                                         real tmax, real& t_out, DHit& h_out, CT& cnt) {
     DRay cur = world;
     DRay rstk[kMaxRayStack];
     int rsp = 0;
@@ -494,12 +515,12 @@ __device__ __forceinline__ bool run_program(const DevScene& S, int pc0, int pc1,
     st.sp = 0;
     THit hit;
     hit.ok = 0;
-    hit.t = 0.0;
+    hit.t = RV(0.0);
     for (int pc = pc0; pc < pc1; ++pc) {
         const DevOp op = S.ops[pc];
-        const rt_node* nd = &S.nodes[op.node];
-        const double lo = op.top == 1 ? tmin : 0.0;
-        const double hi = op.top == 1 ? tmax : RT_INF;
+        const NodeT* nd = &S.nodes[op.node];
+        const real lo = op.top == 1 ? tmin : RV(0.0);
+        const real hi = op.top == 1 ? tmax : RT_INF;
         switch (op.op) {
             case rtamd::OP_XPUSH:
                 cnt.inc(RT_OPC_XFORM);
@@ -535,14 +556,14 @@ __device__ __forceinline__ bool run_program(const DevScene& S, int pc0, int pc1,
                 break;
             }
             case rtamd::OP_LEAF_ISECT: {
-                double t = 0.0;
+                real t = RV(0.0);
                 hit.ok = leaf_intersect(nd, cur, lo, hi, t, hit.h, cnt);
                 hit.t = t;
                 break;
             }
             case rtamd::OP_CSG_ISECT: {   // CSG::intersect (csg.cpp:169-185)
                 const Ivl& v = st.tos;
-                const double t = dmax(v.t0, lo);
+                const real t = dmax(v.t0, lo);
                 hit.ok = v.ok && (t < v.t1 && t < hi);
                 hit.t = t;
                 hit.h = v.h0;
@@ -555,7 +576,7 @@ __device__ __forceinline__ bool run_program(const DevScene& S, int pc0, int pc1,
                 if (hit.ok) {
                     const V3 wp = map_point(nd, hit.h.p);
                     const V3 wn = map_normal(nd, hit.h.n);
-                    const double wt = project_t_world(parent, wp);
+                    const real wt = project_t_world(parent, wp);
                     hit.ok = (wt > lo && wt < hi);
                     hit.h.p = wp;
                     set_face_normal(hit.h, parent, wn);
@@ -597,46 +618,46 @@ constexpr int REF_ORIGIN = 1 << 24;
 
 struct CIvl {
     int ok;
-    double t0, t1;   // interval (event times)
-    double s0, s1;   // t_ref of the entry / exit hit references
+    real t0, t1;   // interval (event times)
+    real s0, s1;   // t_ref of the entry / exit hit references
     int c0, c1;      // codes of the entry / exit hit references
 };
 
 // Primitive::interval for a leaf without computing hit points or normals
 // (geometry.cpp:48-78, 117-147, 207-217).
 template <class CT>
-__device__ __forceinline__ void leaf_ivl_c(const rt_node* nd, int pc, const DRay& r, CIvl& o, CT& cnt) {
+__device__ __forceinline__ void leaf_ivl_c(const NodeT* nd, int pc, const DRay& r, CIvl& o, CT& cnt) {
     o.c0 = pc;
     o.c1 = pc | REF_ROOT1;
     if (nd->kind == RT_NODE_HALFSPACE) {
         cnt.inc(RT_OPC_HALF_IVL);
         const V3 n = ld3(nd->v + 3);
-        const double ndotd = dot3(n, r.d);
+        const real ndotd = dot3(n, r.d);
         V3 diff = v3(r.o.x - nd->v[0], r.o.y - nd->v[1], r.o.z - nd->v[2]);
-        const double f0 = dot3(n, diff);
-        if (__builtin_fabs(ndotd) < 1e-12) {
-            o.ok = f0 >= 0.0;
+        const real f0 = dot3(n, diff);
+        if (fabs_r(ndotd) < RV(1e-12)) {
+            o.ok = f0 >= RV(0.0);
             o.t0 = -RT_INF;
             o.t1 = RT_INF;
         } else {
             o.ok = 1;
-            const double tPlane = -f0 / ndotd;
-            o.t0 = ndotd > 0.0 ? tPlane : -RT_INF;
-            o.t1 = ndotd > 0.0 ? RT_INF : tPlane;
+            const real tPlane = -f0 / ndotd;
+            o.t0 = ndotd > RV(0.0) ? tPlane : -RT_INF;
+            o.t1 = ndotd > RV(0.0) ? RT_INF : tPlane;
         }
     } else {
         cnt.inc(RT_OPC_SPHERE_IVL);
-        const double r0 = nd->v[3];
+        const real r0 = nd->v[3];
         V3 oc = v3(r.o.x - nd->v[0], r.o.y - nd->v[1], r.o.z - nd->v[2]);
-        const double half_b = dot3(oc, r.d);
-        const double cterm = dot3(oc, oc) - r0 * r0;
-        const double disc = half_b * half_b - 1.0 * cterm;
-        o.ok = !(disc < 0.0);
-        const double s = __builtin_sqrt(o.ok ? disc : 0.0);
-        double t0 = (-half_b - s) / 1.0;
-        double t1 = (-half_b + s) / 1.0;
+        const real half_b = dot3(oc, r.d);
+        const real cterm = dot3(oc, oc) - r0 * r0;
+        const real disc = half_b * half_b - RV(1.0) * cterm;
+        o.ok = !(disc < RV(0.0));
+        const real s = sqrt_r(o.ok ? disc : RV(0.0));
+        real t0 = (-half_b - s) / RV(1.0);
+        real t1 = (-half_b + s) / RV(1.0);
         if (t0 > t1) {
-            const double tt = t0;
+            const real tt = t0;
             t0 = t1;
             t1 = tt;
         }
@@ -652,7 +673,7 @@ __device__ __forceinline__ void leaf_ivl_c(const rt_node* nd, int pc, const DRay
 template <class CT>
 __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl& R, CT& cnt) {
     R.ok = 0;
-    R.t0 = R.t1 = R.s0 = R.s1 = 0.0;
+    R.t0 = R.t1 = R.s0 = R.s1 = RV(0.0);
     R.c0 = R.c1 = 0;
     if (!A.ok && !B.ok) return;
     cnt.inc(RT_OPC_CSG_COMBINE);
@@ -666,13 +687,13 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
         const bool useA = A.ok;
         if (op == RT_CSG_INTERSECTION || (op == RT_CSG_DIFFERENCE && !useA)) return;
         const CIvl& X = useA ? A : B;
-        const bool inX = (X.t0 < 1e-6) && (X.t1 > 1e-6);
+        const bool inX = (X.t0 < RV(1e-6)) && (X.t1 > RV(1e-6));
         R.t1 = X.t1;
         R.s1 = X.s1;
         R.c1 = X.c1;
         if (inX) {
             R.ok = __builtin_isfinite(X.t1);
-            R.t0 = 0.0;
+            R.t0 = RV(0.0);
             R.s0 = X.s0;
             R.c0 = (X.c0 & ~REF_FLIP) | REF_ORIGIN;
         } else {
@@ -686,16 +707,16 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
         return;
     }
     // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
-    double et[4];
+    real et[4];
     int ec[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        et[k] = 0.0;
+        et[k] = RV(0.0);
         ec[k] = 0;
     }
     int n = 0;
     {
-        const double tv[4] = {A.t0, A.t1, B.t0, B.t1};
+        const real tv[4] = {A.t0, A.t1, B.t0, B.t1};
         const bool pv[4] = {A.ok && __builtin_isfinite(A.t0), A.ok && __builtin_isfinite(A.t1),
                             B.ok && __builtin_isfinite(B.t0), B.ok && __builtin_isfinite(B.t1)};
 #pragma unroll
@@ -714,7 +735,7 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
 #pragma unroll
     for (int i = 1; i < 4; ++i) {
         if (i < n) {
-            const double vt = et[i];
+            const real vt = et[i];
             const int vc = ec[i];
             if (ev_less(vt, vc, et[0], ec[0])) {
 #pragma unroll
@@ -746,14 +767,14 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
             }
         }
     }
-    bool inA = A.ok && (A.t0 < 1e-6) && (A.t1 > 1e-6);
-    bool inB = B.ok && (B.t0 < 1e-6) && (B.t1 > 1e-6);
+    bool inA = A.ok && (A.t0 < RV(1e-6)) && (A.t1 > RV(1e-6));
+    bool inB = B.ok && (B.t0 < RV(1e-6)) && (B.t1 > RV(1e-6));
     bool inR = csg_combine(op, inA, inB);
     const bool origin = inR;
     bool haveEnter = inR;
     int enterE = -1, exitE = -1;
     bool flipE = false, flipX = false;
-    double tEnt = 0.0, tExt = RT_INF;
+    real tEnt = RV(0.0), tExt = RT_INF;
     const bool originFromA = inA;
     bool done = false;
 #pragma unroll
@@ -834,10 +855,10 @@ template <bool DEEP, class CT>
 __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1, const DRay& r, CT& cnt) {
     CIvl tos, nos;
     tos.ok = nos.ok = 0;
-    tos.t0 = tos.t1 = tos.s0 = tos.s1 = nos.t0 = nos.t1 = nos.s0 = nos.s1 = 0.0;
+    tos.t0 = tos.t1 = tos.s0 = tos.s1 = nos.t0 = nos.t1 = nos.s0 = nos.s1 = RV(0.0);
     tos.c0 = tos.c1 = nos.c0 = nos.c1 = 0;
     constexpr int NSP = DEEP ? kMaxIvlSpill : 1;
-    double sp_t0[NSP], sp_t1[NSP], sp_s0[NSP], sp_s1[NSP];
+    real sp_t0[NSP], sp_t1[NSP], sp_s0[NSP], sp_s1[NSP];
     int sp_ok[NSP], sp_c0[NSP], sp_c1[NSP];
     int sp = 0;   // stack entries (wave-uniform)
     const FRay fr = to_fray(r);
@@ -860,7 +881,7 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
                 cnt.inc(RT_OPC_CULLED);
                 CIvl e, v;
                 e.ok = 0;
-                e.t0 = e.t1 = e.s0 = e.s1 = 0.0;
+                e.t0 = e.t1 = e.s0 = e.s1 = RV(0.0);
                 e.c0 = e.c1 = 0;
                 csg_c(op.csg_op, tos, e, v, cnt);
                 tos = v;
@@ -883,13 +904,13 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
 
 // Leaf Primitive::intersect without normal (t and acceptance only).
 template <class CT>
-__device__ __forceinline__ bool leaf_hit_t(const rt_node* nd, const DRay& r, double tmin, double tmax, double& t,
+__device__ __forceinline__ bool leaf_hit_t(const NodeT* nd, const DRay& r, real tmin, real tmax, real& t,
                                            CT& cnt) {
     if (nd->kind == RT_NODE_HALFSPACE) {   // geometry.cpp:90-106
         cnt.inc(RT_OPC_HALF_ISECT);
         const V3 n = ld3(nd->v + 3);
-        const double ndotd = dot3(n, r.d);
-        if (__builtin_fabs(ndotd) < 1e-12) return false;
+        const real ndotd = dot3(n, r.d);
+        if (fabs_r(ndotd) < RV(1e-12)) return false;
         V3 diff = v3(nd->v[0] - r.o.x, nd->v[1] - r.o.y, nd->v[2] - r.o.z);
         t = dot3(n, diff) / ndotd;
         const bool ok = !(t < tmin || t > tmax);
@@ -897,16 +918,16 @@ __device__ __forceinline__ bool leaf_hit_t(const rt_node* nd, const DRay& r, dou
         return ok;
     }
     cnt.inc(RT_OPC_SPHERE_ISECT);   // geometry.cpp:12-37
-    const double rad = nd->v[3];
+    const real rad = nd->v[3];
     V3 oc = v3(r.o.x - nd->v[0], r.o.y - nd->v[1], r.o.z - nd->v[2]);
-    const double half_b = dot3(oc, r.d);
-    const double cterm = dot3(oc, oc) - rad * rad;
-    const double disc = half_b * half_b - 1.0 * cterm;
-    if (disc < 0.0) return false;
-    const double sq = __builtin_sqrt(disc);
-    t = (-half_b - sq) / 1.0;
+    const real half_b = dot3(oc, r.d);
+    const real cterm = dot3(oc, oc) - rad * rad;
+    const real disc = half_b * half_b - RV(1.0) * cterm;
+    if (disc < RV(0.0)) return false;
+    const real sq = sqrt_r(disc);
+    t = (-half_b - sq) / RV(1.0);
     if (t < tmin || t > tmax) {
-        t = (-half_b + sq) / 1.0;
+        t = (-half_b + sq) / RV(1.0);
         if (t < tmin || t > tmax) return false;
     }
     cnt.inc(RT_OPC_SPHERE_ISECT_HIT);
@@ -915,13 +936,13 @@ __device__ __forceinline__ bool leaf_hit_t(const rt_node* nd, const DRay& r, dou
 
 // Normal / front_face / material of a leaf hit at point p on frame ray r.
 template <class CT>
-__device__ __forceinline__ void leaf_shading(const rt_node* nd, const DRay& r, V3 p, DHit& h, CT& cnt) {
+__device__ __forceinline__ void leaf_shading(const NodeT* nd, const DRay& r, V3 p, DHit& h, CT& cnt) {
     if (nd->kind == RT_NODE_HALFSPACE) {
         set_face_normal(h, r, ld3(nd->v + 3));
         h.mat = nd->mat;
         return;
     }
-    const double rad = nd->v[3];
+    const real rad = nd->v[3];
     const V3 outward = v3((p.x - nd->v[0]) / rad, (p.y - nd->v[1]) / rad, (p.z - nd->v[2]) / rad);
     set_face_normal(h, r, outward);
     h.mat = nd->kind == RT_NODE_SPHERE ? nd->mat : pick_region(nd, p, cnt);
@@ -929,13 +950,13 @@ __device__ __forceinline__ void leaf_shading(const rt_node* nd, const DRay& r, V
 
 // Resolve a compact hit reference on frame ray r into (n, ff, mat).
 template <class CT>
-__device__ __forceinline__ void resolve_ref(const DevScene& S, const DRay& r, double ts, int code, DHit& h,
+__device__ __forceinline__ void resolve_ref(const DevScene& S, const DRay& r, real ts, int code, DHit& h,
                                             CT& cnt) {
-    const rt_node* nd = &S.nodes[S.ops[code & REF_PC_MASK].node];
+    const NodeT* nd = &S.nodes[S.ops[code & REF_PC_MASK].node];
     const V3 p = __builtin_isfinite(ts) ? ray_at(r, ts) : r.o;
     leaf_shading(nd, r, p, h, cnt);
     if (code & REF_ORIGIN) {
-        h.n = v3(0.0, 0.0, 0.0);
+        h.n = v3(RV(0.0), RV(0.0), RV(0.0));
         h.ff = 1;
     }
     if (code & REF_FLIP) h.ff = 0;
@@ -952,8 +973,8 @@ __device__ __forceinline__ DRay chain_ray(const DevScene& S, int pc0, int k, con
 // Primitive::intersect(object, ray, tmin, tmax): hit t, hit point p and a lazy
 // reference (ts, code) resolved later by resolve_hit().
 template <bool EAGER, bool DEEP, class CT>
-__device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, const DRay& world, double tmin,
-                                           double tmax, double& t, V3& p, double& ts, int& code, CT& cnt) {
+__device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, const DRay& world, real tmin,
+                                           real tmax, real& t, V3& p, real& ts, int& code, CT& cnt) {
     if (ob.kind <= rtamd::OBJ_POKE) {
         const bool ok = leaf_hit_t(&S.nodes[ob.node], world, tmin, tmax, t, cnt);
         p = ray_at(world, t);
@@ -968,8 +989,8 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
             cnt.inc(RT_OPC_XFORM);
             cur = local_ray(&S.nodes[S.ops[ob.pc0 + k].node], cur);
         }
-        const double lo = ob.m ? 0.0 : tmin;
-        const double hi = ob.m ? RT_INF : tmax;
+        const real lo = ob.m ? RV(0.0) : tmin;
+        const real hi = ob.m ? RT_INF : tmax;
         bool ok;
         if (ob.core == 0) {
             ok = leaf_hit_t(&S.nodes[ob.node], cur, lo, hi, t, cnt);
@@ -986,10 +1007,10 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
         }
         for (int k = ob.m - 1; k >= 0; --k) {
             const DRay parent = (k == 0) ? world : chain_ray(S, ob.pc0, k, world);
-            const rt_node* nd = &S.nodes[S.ops[ob.pc0 + k].node];
+            const NodeT* nd = &S.nodes[S.ops[ob.pc0 + k].node];
             const V3 wp = map_point(nd, p);
-            const double wt = project_t_world(parent, wp);
-            const double l = k ? 0.0 : tmin, h = k ? RT_INF : tmax;
+            const real wt = project_t_world(parent, wp);
+            const real l = k ? RV(0.0) : tmin, h = k ? RT_INF : tmax;
             ok = ok && (wt > l && wt < h);
             p = wp;
             t = wt;
@@ -1011,8 +1032,8 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
 
 // Full hit record (p, n, front_face, mat) of the winning object.
 template <bool EAGER, class CT>
-__device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DRay& world, double tmin, V3 p,
-                                            double ts, int code, DHit& h, CT& cnt) {
+__device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DRay& world, real tmin, V3 p,
+                                            real ts, int code, DHit& h, CT& cnt) {
     const DevObj ob = S.objs[obj];
     h.p = p;
     if (ob.kind <= rtamd::OBJ_POKE) {
@@ -1031,7 +1052,7 @@ __device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DR
         return;
     }
     if constexpr (EAGER) {   // re-run the eager program (result does not depend on tmax)
-        double t;
+        real t;
         run_program<EAGER>(S, ob.pc0, ob.pc1, world, tmin, RT_INF, t, h, cnt);
         h.p = p;
     }
@@ -1041,12 +1062,12 @@ __device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DR
 // own accept rule with tmax = closest-so-far, so ties resolve as in the
 // reference (Sphere/HalfSpace accept t == tmax, CSG/transforms do not).
 template <bool EAGER, bool DEEP, class CT>
-__device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, double tmax, double& t_best,
+__device__ bool scene_intersect(const DevScene& S, const DRay& r, real tmin, real tmax, real& t_best,
                                 DHit& best, CT& cnt) {
-    double closest = tmax;
+    real closest = tmax;
     int win = -1;
-    V3 wp = v3(0.0, 0.0, 0.0);
-    double wts = 0.0;
+    V3 wp = v3(RV(0.0), RV(0.0), RV(0.0));
+    real wts = RV(0.0);
     int wcode = 0;
     const FRay fr = to_fray(r);
     const float ftmin = (float)tmin;
@@ -1062,7 +1083,7 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
             }
         }
         if (ob.kind == rtamd::OBJ_GROUP) continue;
-        double t = 0.0, ts = 0.0;
+        real t = RV(0.0), ts = RV(0.0);
         V3 p;
         int code = 0;
         if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt)) {
@@ -1081,7 +1102,7 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, double tmin, d
 
 // Scene::occluded (scene.cpp:33-42): any hit; per-lane early exit.
 template <bool EAGER, bool DEEP, class CT>
-__device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, double tmax, CT& cnt) {
+__device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real tmax, CT& cnt) {
     bool hit = false;
     const FRay fr = to_fray(r);
     const float ftmin = (float)tmin, ftmax = (float)tmax;
@@ -1098,7 +1119,7 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, do
         }
         if (ob.kind == rtamd::OBJ_GROUP) continue;
         if (!hit) {
-            double t = 0.0, ts = 0.0;
+            real t = RV(0.0), ts = RV(0.0);
             V3 p;
             int code = 0;
             hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
@@ -1109,7 +1130,7 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, double tmin, do
 
 // ----------------------------------------------------------------- shading
 __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
-    return v3(1.0 - (1.0 - a.x) * (1.0 - b.x), 1.0 - (1.0 - a.y) * (1.0 - b.y), 1.0 - (1.0 - a.z) * (1.0 - b.z));
+    return v3(RV(1.0) - (RV(1.0) - a.x) * (RV(1.0) - b.x), RV(1.0) - (RV(1.0) - a.y) * (RV(1.0) - b.y), RV(1.0) - (RV(1.0) - a.z) * (RV(1.0) - b.z));
 }
 
 // shade_lambert_phong (shading.cpp:31-138), point lights only (the loader
@@ -1117,44 +1138,44 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 // DL: the scene may have directional lights (the lean kernels, chosen only
 // for scenes without, do not carry their code or registers).
 template <bool EAGER, bool DEEP, bool DL, class CT>
-__device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
-    if (hit.mat < 0) return v3(1.0, 0.0, 1.0);
+__device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
+    if (hit.mat < 0) return v3(RV(1.0), RV(0.0), RV(1.0));
     cnt.inc(RT_OPC_SHADE_CALL);
     const V3 n = hit.n;
-    const double eps = dmax(1e-3, 1e-4 * ht);
+    const real eps = dmax(RV(1e-3), RV(1e-4) * ht);
     // Two passes over the lights so that only (p, n, eps) stay live across
     // the shadow queries (register pressure): pass 1 decides, per light, the
     // reference's early-outs and the occlusion query; pass 2 recomputes the
     // same light geometry (identical operations, identical bits) and
     // accumulates in the reference's order.  Lights beyond 32 are handled in
     // further rounds of the same two passes.
-    V3 E = v3(0.0, 0.0, 0.0);
+    V3 E = v3(RV(0.0), RV(0.0), RV(0.0));
     {
-        const rt_material* m = &S.mats[hit.mat];
+        const MatT* m = &S.mats[hit.mat];
         E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
     }
     // directional lights first (shading.cpp:45-76): no falloff, shadow ray to infinity
     for (int li = 0; DL && li < S.n_dlights; ++li) {
-        const rt_dir_light* L = &S.dlights[li];
+        const DLightT* L = &S.dlights[li];
         cnt.inc(RT_OPC_LIGHT_EVAL);
         const V3 wi = normalized(v3(-L->dir[0], -L->dir[1], -L->dir[2]));
-        const double ndotl = dmax(0.0, dot3(n, wi));
-        if (ndotl <= 0.0) continue;
+        const real ndotl = dmax(RV(0.0), dot3(n, wi));
+        if (ndotl <= RV(0.0)) continue;
         const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
         ++n_occl;
         if (scene_occluded<EAGER, DEEP>(S, make_ray(so, wi), eps, RT_INF, cnt)) continue;
         cnt.inc(RT_OPC_SHADE_LIGHT);
-        const rt_material* m = &S.mats[hit.mat];
-        const double sd = m->kd * ndotl;   // scale(mul(albedo, radiance), kd * ndotl)
+        const MatT* m = &S.mats[hit.mat];
+        const real sd = m->kd * ndotl;   // scale(mul(albedo, radiance), kd * ndotl)
         const V3 Ed = v3(m->albedo[0] * L->radiance[0] * sd, m->albedo[1] * L->radiance[1] * sd,
                          m->albedo[2] * L->radiance[2] * sd);
-        V3 Es = v3(0.0, 0.0, 0.0);
-        if (m->ks > 0.0) {
+        V3 Es = v3(RV(0.0), RV(0.0), RV(0.0));
+        if (m->ks > RV(0.0)) {
             cnt.inc(RT_OPC_SHADE_SPEC);
-            const V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
-                                        2.0 * dot3(n, wi) * n.z - wi.z));
-            const double rdotv = dmax(0.0, dot3(rr, wo));
-            const double spec = pow(rdotv, m->shininess) * m->ks;
+            const V3 rr = normalized(v3(RV(2.0) * dot3(n, wi) * n.x - wi.x, RV(2.0) * dot3(n, wi) * n.y - wi.y,
+                                        RV(2.0) * dot3(n, wi) * n.z - wi.z));
+            const real rdotv = dmax(RV(0.0), dot3(rr, wo));
+            const real spec = pow(rdotv, m->shininess) * m->ks;
             Es = v3(L->radiance[0] * spec, L->radiance[1] * spec, L->radiance[2] * spec);
         }
         E = combine(E, combine(Ed, Es));
@@ -1163,16 +1184,16 @@ __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32
         const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
         uint32_t lit = 0;
         for (int li = l0; li < l1; ++li) {
-            const rt_light* L = &S.lights[li];
+            const LightT* L = &S.lights[li];
             cnt.inc(RT_OPC_LIGHT_EVAL);
             V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
-            double d2 = dot3(tl, tl);
-            if (d2 <= 0.01) d2 = 0.01;
-            const double dist = __builtin_sqrt(d2);
+            real d2 = dot3(tl, tl);
+            if (d2 <= RV(0.01)) d2 = RV(0.01);
+            const real dist = sqrt_r(d2);
             const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
-            const double ndotl = dmax(0.0, dot3(n, wi));
-            if (ndotl <= 0.0) continue;
-            const double max_t = dist - eps;
+            const real ndotl = dmax(RV(0.0), dot3(n, wi));
+            if (ndotl <= RV(0.0)) continue;
+            const real max_t = dist - eps;
             if (max_t <= eps) continue;
             const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
             const DRay sr = make_ray(so, wi);
@@ -1181,40 +1202,40 @@ __device__ V3 shade(const DevScene& S, double ht, const DHit& hit, V3 wo, uint32
             lit |= 1u << (li - l0);
         }
         if (!lit) continue;
-        const rt_material* m = &S.mats[hit.mat];
-        const double kd = m->kd, ks = m->ks, shin = m->shininess;
+        const MatT* m = &S.mats[hit.mat];
+        const real kd = m->kd, ks = m->ks, shin = m->shininess;
         const V3 alb = ld3(m->albedo);
         for (int li = l0; li < l1; ++li) {
             if (!((lit >> (li - l0)) & 1u)) continue;
-            const rt_light* L = &S.lights[li];
+            const LightT* L = &S.lights[li];
             V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
-            double d2 = dot3(tl, tl);
-            if (d2 <= 0.01) d2 = 0.01;
-            const double dist = __builtin_sqrt(d2);
+            real d2 = dot3(tl, tl);
+            if (d2 <= RV(0.01)) d2 = RV(0.01);
+            const real dist = sqrt_r(d2);
             const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
-            const double ndotl = dmax(0.0, dot3(n, wi));
+            const real ndotl = dmax(RV(0.0), dot3(n, wi));
             cnt.inc(RT_OPC_SHADE_LIGHT);
-            const double ed = dmax(0.5, dist);
-            const double falloff = 1.0 / (ed * ed);
-            const double f2 = falloff * 2.0;
+            const real ed = dmax(RV(0.5), dist);
+            const real falloff = RV(1.0) / (ed * ed);
+            const real f2 = falloff * RV(2.0);
             const V3 IL = v3(L->intensity[0] * f2, L->intensity[1] * f2, L->intensity[2] * f2);
-            const double sd = kd * ndotl * 1.5;
+            const real sd = kd * ndotl * RV(1.5);
             const V3 Ed = v3(alb.x * IL.x * sd, alb.y * IL.y * sd, alb.z * IL.z * sd);
-            V3 Es = v3(0.0, 0.0, 0.0);
-            if (ks > 0.0) {
+            V3 Es = v3(RV(0.0), RV(0.0), RV(0.0));
+            if (ks > RV(0.0)) {
                 cnt.inc(RT_OPC_SHADE_SPEC);
-                const V3 rr = normalized(v3(2.0 * dot3(n, wi) * n.x - wi.x, 2.0 * dot3(n, wi) * n.y - wi.y,
-                                            2.0 * dot3(n, wi) * n.z - wi.z));
-                const double rdotv = dmax(0.0, dot3(rr, wo));
-                const double spec = pow(rdotv, shin) * ks;
+                const V3 rr = normalized(v3(RV(2.0) * dot3(n, wi) * n.x - wi.x, RV(2.0) * dot3(n, wi) * n.y - wi.y,
+                                            RV(2.0) * dot3(n, wi) * n.z - wi.z));
+                const real rdotv = dmax(RV(0.0), dot3(rr, wo));
+                const real spec = pow(rdotv, shin) * ks;
                 Es = v3(IL.x * spec, IL.y * spec, IL.z * spec);
             }
             E = combine(E, combine(Ed, Es));
         }
     }
-    E.x = dmin(1.5, E.x);
-    E.y = dmin(1.5, E.y);
-    E.z = dmin(1.5, E.z);
+    E.x = dmin(RV(1.5), E.x);
+    E.y = dmin(RV(1.5), E.y);
+    E.z = dmin(RV(1.5), E.z);
     return E;
 }
 
@@ -1233,11 +1254,11 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
     if constexpr (!SECONDARY) {
         // No material reflects or refracts (or recursion <= 1): trace_recursive
         // reduces to one closest hit + local shading (tracer.cpp:22-37, 72).
-        if (S.rec_limit <= 0) return v3(0.0, 0.0, 0.0);
-        double ht = 0.0;
+        if (S.rec_limit <= 0) return v3(RV(0.0), RV(0.0), RV(0.0));
+        real ht = RV(0.0);
         DHit h;
         ++n_isect;
-        if (!scene_intersect<EAGER, DEEP>(S, r, 1e-4, RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+        if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
         return shade<EAGER, DEEP, DL>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
     }
     Frame stk[kMaxDepth];
@@ -1249,12 +1270,12 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         // ---- evaluate node (r, depth)
         bool descend = false;
         if (depth >= limit) {
-            ret = v3(0.0, 0.0, 0.0);
+            ret = v3(RV(0.0), RV(0.0), RV(0.0));
         } else {
-            double ht = 0.0;
+            real ht = RV(0.0);
             DHit h;
             ++n_isect;
-            if (!scene_intersect<EAGER, DEEP>(S, r, 1e-4, RT_INF, ht, h, cnt)) {
+            if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) {
                 ret = v3(S.bg[0], S.bg[1], S.bg[2]);
             } else {
                 const V3 wo = normalized(vneg(r.d));
@@ -1262,25 +1283,25 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
                 if (h.mat < 0) {
                     ret = direct;
                 } else {
-                    const rt_material* mat = &S.mats[h.mat];
+                    const MatT* mat = &S.mats[h.mat];
                     const bool can = depth < limit - 1;
-                    const bool want_refl = mat->kr > 0.0 && can;
+                    const bool want_refl = mat->kr > RV(0.0) && can;
                     bool want_refr = false;
                     DRay refr;
-                    if (mat->kt > 0.0 && can) {
-                        const double eta = h.ff ? (S.medium_index / mat->refractive_index)
+                    if (mat->kt > RV(0.0) && can) {
+                        const real eta = h.ff ? (S.medium_index / mat->refractive_index)
                                                 : (mat->refractive_index / S.medium_index);
                         const V3 inc = normalized(r.d);
-                        const double cos_i = -dot3(inc, h.n);   // tracer.cpp:100-104
-                        const double st2 = eta * eta * dmax(0.0, 1.0 - cos_i * cos_i);
-                        if (!(st2 >= 1.0)) {
+                        const real cos_i = -dot3(inc, h.n);   // tracer.cpp:100-104
+                        const real st2 = eta * eta * dmax(RV(0.0), RV(1.0) - cos_i * cos_i);
+                        if (!(st2 >= RV(1.0))) {
                             want_refr = true;
-                            const double cos_t = __builtin_sqrt(1.0 - st2);   // tracer.cpp:87-98
-                            const double k = eta * cos_i - cos_t;
+                            const real cos_t = sqrt_r(RV(1.0) - st2);   // tracer.cpp:87-98
+                            const real k = eta * cos_i - cos_t;
                             const V3 rd = normalized(v3(inc.x * eta + h.n.x * k, inc.y * eta + h.n.y * k,
                                                         inc.z * eta + h.n.z * k));
-                            const V3 ro = h.ff ? v3(h.p.x - h.n.x * 1e-6, h.p.y - h.n.y * 1e-6, h.p.z - h.n.z * 1e-6)
-                                               : v3(h.p.x + h.n.x * 1e-6, h.p.y + h.n.y * 1e-6, h.p.z + h.n.z * 1e-6);
+                            const V3 ro = h.ff ? v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6))
+                                               : v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6));
                             refr = make_ray(ro, rd);
                         }
                     }
@@ -1293,10 +1314,10 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
                         if (want_refl) {
                             cnt.inc(RT_OPC_SECONDARY);
                             const V3 inc = normalized(r.d);
-                            const double k = 2.0 * dot3(inc, h.n);   // reflect (tracer.cpp:76-78)
+                            const real k = RV(2.0) * dot3(inc, h.n);   // reflect (tracer.cpp:76-78)
                             const V3 rd = normalized(v3(inc.x - h.n.x * k, inc.y - h.n.y * k, inc.z - h.n.z * k));
-                            const V3 ro = h.ff ? v3(h.p.x + h.n.x * 1e-6, h.p.y + h.n.y * 1e-6, h.p.z + h.n.z * 1e-6)
-                                               : v3(h.p.x - h.n.x * 1e-6, h.p.y - h.n.y * 1e-6, h.p.z - h.n.z * 1e-6);
+                            const V3 ro = h.ff ? v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6))
+                                               : v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6));
                             f.stage = 0;
                             stk[sp++] = f;
                             r = make_ray(ro, rd);
@@ -1319,7 +1340,7 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         bool resumed = false;
         while (sp > 0) {
             Frame& f = stk[sp - 1];
-            const rt_material* mat = &S.mats[f.mat];
+            const MatT* mat = &S.mats[f.mat];
             if (f.stage == 0) {
                 f.total = combine(f.total, v3(ret.x * mat->kr, ret.y * mat->kr, ret.z * mat->kr));
                 if (f.want_refr) {
@@ -1344,10 +1365,10 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
 
 // ------------------------------------------------------------------ camera
 // Camera::generate_ray_subpixel (camera.h:68-78)
-__device__ __forceinline__ DRay gen_ray_subpixel(const DevScene& S, int i, int j, double dx, double dy) {
-    const double sx = (i + 0.5 + dx) / (double)S.cam_nx;
-    const double sy = (j + 0.5 + dy) / (double)S.cam_ny;
-    const V3 Sp = v3(S.P[0] + S.Lx * sx + 0.0 * sy, S.P[1] + 0.0 * sx + S.Ly * sy, S.P[2] + 0.0 * sx + 0.0 * sy);
+__device__ __forceinline__ DRay gen_ray_subpixel(const DevScene& S, int i, int j, real dx, real dy) {
+    const real sx = (i + RV(0.5) + dx) / (real)S.cam_nx;
+    const real sy = (j + RV(0.5) + dy) / (real)S.cam_ny;
+    const V3 Sp = v3(S.P[0] + S.Lx * sx + RV(0.0) * sy, S.P[1] + RV(0.0) * sx + S.Ly * sy, S.P[2] + RV(0.0) * sx + RV(0.0) * sy);
     const V3 e = ld3(S.eye);
     return make_ray(e, normalized(v3(Sp.x - e.x, Sp.y - e.y, Sp.z - e.z)));
 }
@@ -1356,12 +1377,12 @@ __device__ __forceinline__ DRay gen_ray_subpixel(const DevScene& S, int i, int j
 __device__ __forceinline__ DRay gen_ray(const DevScene& S, int i, int j) {
     const int nx = S.cam_nx, ny = S.cam_ny;
     const V3 e = ld3(S.eye);
-    if (i < 0 || i >= nx || j < 0 || j >= ny) return make_ray(e, v3(0.0, 0.0, -1.0));
-    const double sx = ((double)i + 0.5) / (double)nx;
+    if (i < 0 || i >= nx || j < 0 || j >= ny) return make_ray(e, v3(RV(0.0), RV(0.0), -RV(1.0)));
+    const real sx = ((real)i + RV(0.5)) / (real)nx;
     const int jf = ny - 1 - j;
-    const double sy = ((double)jf + 0.5) / (double)ny;
-    const V3 Sp = v3(S.P[0] + S.Lx * sx + 0.0 * sy, S.P[1] + 0.0 * sx + S.Ly * sy, S.P[2] + 0.0 * sx + 0.0 * sy);
+    const real sy = ((real)jf + RV(0.5)) / (real)ny;
+    const V3 Sp = v3(S.P[0] + S.Lx * sx + RV(0.0) * sy, S.P[1] + RV(0.0) * sx + S.Ly * sy, S.P[2] + RV(0.0) * sx + RV(0.0) * sy);
     return make_ray(e, normalized(v3(Sp.x - e.x, Sp.y - e.y, Sp.z - e.z)));
 }
 
-}  // namespace rtd
+}  // namespace RT_NS

@@ -1,0 +1,314 @@
+// rt_kernels.hpp — the render kernels, built once per precision right after
+// rt_device.hpp (RT_NS = rtd: FP64 parity path, rt_render.hip; RT_NS = rtf:
+// FP32 fast path, rt_render_f32.hip).
+//
+// Standard mode (Tracer::render, tracer.cpp:282-300):
+//   k_std: one lane per (pixel, sample); a wave covers 4x2 pixels x 8 samples,
+//   a 256-thread block 8x4 pixels.  Samples are summed in order s = 0..7
+//   across the 8 lanes of a pixel (cross-lane shuffles), then x 1/8.
+// Paper mode (tracer.cpp:258-281):
+//   k_paper_primary: one lane per pixel: the primary intersect (shared by
+//   trace_paper, the centre probe and the four neighbour probes of
+//   get_edge_strength, which all re-trace identical rays) + shading.
+//   k_paper_finish: edge strength from the stored neighbour hits + hatch.
+// The framebuffer, jitter draws and paper hit records stay double in both
+// precisions (the float kernels convert on load / store).
+
+namespace RT_NS {
+
+using rtamd::kCounterSlots;
+using rtamd::kCounterWords;
+using rtamd::PaperParams;
+using rtamd::SceneView;
+using rtamd::StdParams;
+
+namespace {
+
+// Ray / op counters: wave reduction by shuffles, block reduction through LDS,
+// then one atomic per block and counter into one of kCounterSlots slots
+// (blockIdx-hashed).  A single hot address would serialize ~2M atomics at the
+// L2 (~6 ns each, MI355X_MICROARCH.md fan-in row) - 12 ms per 4K frame.
+template <bool C>
+__device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
+    constexpr int NW = C ? 18 : 2;
+    __shared__ unsigned long long red[4][NW];
+    unsigned long long v[NW];
+    v[0] = ni;
+    v[1] = no;
+    if constexpr (C) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[2 + k] = cnt.c[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NW; ++k) red[wave][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < NW) {
+        const unsigned long long sum = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                       red[3][threadIdx.x];
+        const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x) % kCounterSlots;
+        if (sum) atomicAdd(&ctr[(size_t)slot * kCounterWords + threadIdx.x], sum);
+    }
+}
+
+// Occupancy target of the lean variants (E = D = SEC = false): 4 waves/SIMD
+// caps them at 128 VGPRs; the few values the compiler then spills are
+// long-lived (stored once, reloaded once), and the extra wave per SIMD hides
+// FP64 latency (measured 21.6 -> 19.2 ms on config 4; 5 and 6 are slower).
+#ifndef RT_LEAN_WAVES
+#define RT_LEAN_WAVES 4
+#endif
+
+template <bool E, bool D, bool SEC, bool C, bool DL = true>
+__device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int s = lane & 7;
+    const int pix = lane >> 3;
+    const int x = blockIdx.x * 8 + (wave & 1) * 4 + (pix & 3);
+    const int ri = blockIdx.y * 4 + (wave >> 1) * 2 + (pix >> 2);
+    const bool active = x < P.W && ri < P.n_rows;
+    uint32_t ni = 0, no = 0;
+    Cnt<C> cnt;
+    V3 c = v3(RV(0.0), RV(0.0), RV(0.0));
+    if (active) {
+        const int r = P.rows[ri];
+        const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
+        // draws 16p+2s, 16p+2s+1 of the stream: dx, dy (tracer.cpp:293)
+        const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)P.jrow[ri] * P.W + x) * 16 + 2 * s);
+        const DRay ray = gen_ray_subpixel(S, x, y, RV(j.x), RV(j.y));
+        c = trace<E, D, SEC, DL>(S, ray, ni, no, cnt);
+    }
+    // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
+    const int base = lane & ~7;
+    V3 acc = v3(RV(0.0), RV(0.0), RV(0.0));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const real cx = __shfl(c.x, base + k);
+        const real cy = __shfl(c.y, base + k);
+        const real cz = __shfl(c.z, base + k);
+        acc.x += cx;
+        acc.y += cy;
+        acc.z += cz;
+    }
+    if (active && s == 0) {
+        const real inv = RV(1.0) / (real)8;
+        double* o = P.fb + ((size_t)ri * P.W + x) * 3;
+        o[0] = acc.x * inv;
+        o[1] = acc.y * inv;
+        o[2] = acc.z * inv;
+    }
+    flush_counters(P.counters, ni, no, cnt);
+}
+
+template <bool E, bool D, bool SEC, bool C>
+__global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
+    std_body<E, D, SEC, C>(S, P);
+}
+
+template <bool C>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
+                                                                                                       StdParams P) {
+    std_body<false, false, false, C, false>(S, P);
+}
+
+template <bool E, bool D, bool C, bool DL = true>
+__device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
+    // block 16x16 pixels, wave 8x8
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const bool active = x < P.W && li < P.n_list;
+    uint32_t ni = 0, no = 0;
+    Cnt<C> cnt;
+    if (active) {
+        const int ei = P.ext_list[li];
+        const int y = P.ext_rows[ei];
+        const DRay r = gen_ray(S, x, y);
+        real ht = RV(0.0);
+        DHit h;
+        ++ni;
+        const bool hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
+        const size_t idx = (size_t)ei * P.W + x;
+        P.hit[idx] = hits ? 1 : 0;
+        P.t[idx] = ht;
+        P.nx[idx] = h.n.x;
+        P.ny[idx] = h.n.y;
+        P.nz[idx] = h.n.z;
+        P.mat[idx] = hits ? h.mat : -3;
+        if (P.ext_shade[ei]) {
+            // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
+            V3 base = v3(RV(1.0), RV(1.0), RV(1.0));
+            if (hits) base = shade<E, D, DL>(S, ht, h, normalized(vneg(r.d)), no, cnt);
+            P.lum[idx] = RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z;
+        }
+    }
+    flush_counters(P.counters, ni, no, cnt);
+}
+
+template <bool E, bool D, bool C>
+__global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
+    paper_primary_body<E, D, C>(S, P);
+}
+
+template <bool C>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
+    DevScene S, PaperParams P) {
+    paper_primary_body<false, false, C, false>(S, P);
+}
+
+// apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
+__device__ __forceinline__ real crosshatch(real lum, int x, int y) {
+    if (lum < RV(0.15)) return RV(0.0);
+    const real darkness = RV(1.0) - lum;
+    const bool diag1 = ((x + y) % 4) < 1;
+    const bool diag2 = ((x - y) % 4) < 1;
+    const bool horizontal = (y % 4) < 1;
+    bool draw = false;
+    if (darkness > RV(0.8)) draw = (diag1 && diag2) || horizontal;
+    else if (darkness > RV(0.65)) draw = (diag1 && diag2) || (horizontal && ((x + y) % 3 == 0));
+    else if (darkness > RV(0.5)) draw = (diag1 && diag2) || (horizontal && ((x + y) % 4 == 0));
+    else if (darkness > RV(0.35)) draw = diag1 || (horizontal && ((x + y) % 3 == 0));
+    else if (darkness > RV(0.2)) draw = diag1;
+    else if (darkness > RV(0.12)) draw = diag1 && ((x + y) % 8) < 2;
+    return draw ? RV(0.0) : RV(1.0);
+}
+
+__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= P.W || ri >= P.n_rows) return;
+    const int y = P.rows[ri];
+    const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
+    const size_t ci = (size_t)e_c * P.W + x;
+    const bool ch = P.hit[ci] != 0;
+    const real ct = P.t[ci];
+    const V3 cn = v3(P.nx[ci], P.ny[ci], P.nz[ci]);
+    const int cm = P.mat[ci];
+    // get_edge_strength (tracer.cpp:133-178): neighbours (-1,0) (1,0) (0,-1) (0,1)
+    real maxEdge = RV(0.0);
+    int valid = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int dx = (i == 0) ? -1 : (i == 1) ? 1 : 0;
+        const int dy = (i == 2) ? -1 : (i == 3) ? 1 : 0;
+        const int nxp = x + dx, nyp = y + dy;
+        if (nxp < 0 || nxp >= P.W || nyp < 0 || nyp >= P.H) continue;
+        ++valid;
+        const int er = (dy < 0) ? e_up : (dy > 0) ? e_dn : e_c;
+        const size_t ni = (size_t)er * P.W + nxp;
+        const bool nh = P.hit[ni] != 0;
+        if (ch != nh) {
+            maxEdge = dmax(maxEdge, RV(0.9));
+            continue;
+        }
+        if (ch && nh) {
+            const real nt = P.t[ni];
+            const real minD = dmin(ct, nt), maxD = dmax(ct, nt);
+            if (minD > RV(1e-4) && maxD / minD > RV(3.0)) maxEdge = dmax(maxEdge, RV(0.6));
+            const real nd = dot3(cn, v3(P.nx[ni], P.ny[ni], P.nz[ni]));
+            if (nd < RV(0.2)) maxEdge = dmax(maxEdge, RV(0.5));
+            if (cm != P.mat[ni] && nd < RV(0.7)) maxEdge = dmax(maxEdge, RV(0.3));
+        }
+    }
+    if (valid < 4) maxEdge *= RV(0.5);
+    const real edge = maxEdge;
+    V3 o;
+    if (edge > RV(0.8)) {
+        o = v3(RV(0.0), RV(0.0), RV(0.0));
+    } else if (edge > RV(0.5)) {
+        o = v3(RV(0.2), RV(0.2), RV(0.2));
+    } else {
+        const real h = crosshatch(P.lum[ci], x, y);
+        o = v3(h, h, h);
+        if (edge > RV(0.3)) {
+            const real darken = (edge - RV(0.3)) * RV(0.4);
+            o.x *= (RV(1.0) - darken);
+            o.y *= (RV(1.0) - darken);
+            o.z *= (RV(1.0) - darken);
+        }
+    }
+    double* dst = P.fb + ((size_t)ri * P.W + x) * 3;
+    dst[0] = o.x;
+    dst[1] = o.y;
+    dst[2] = o.z;
+}
+
+DevScene make_scene(const SceneView& V) {
+    DevScene S;
+    S.nodes = static_cast<const NodeT*>(V.nodes);
+    S.mats = static_cast<const MatT*>(V.mats);
+    S.lights = static_cast<const LightT*>(V.lights);
+    S.dlights = static_cast<const DLightT*>(V.dlights);
+    S.objs = V.objs;
+    S.ops = V.ops;
+    S.gb = V.gb;
+    S.n_lights = V.n_lights;
+    S.n_dlights = V.n_dlights;
+    S.n_objs = V.n_objs;
+    S.cam_nx = V.cam_nx;
+    S.cam_ny = V.cam_ny;
+    S.rec_limit = V.rec_limit;
+    S.cull = V.cull;
+    for (int i = 0; i < 3; ++i) {
+        S.eye[i] = (real)V.eye[i];
+        S.P[i] = (real)V.P[i];
+        S.bg[i] = (real)V.bg[i];
+        S.amb[i] = (real)V.amb[i];
+    }
+    S.Lx = (real)V.Lx;
+    S.Ly = (real)V.Ly;
+    S.medium_index = (real)V.medium_index;
+    return S;
+}
+
+template <bool E, bool D, bool SEC>
+void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
+    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_std<E, D, SEC, false>), grid, dim3(256), 0, st, S, P);
+}
+
+template <bool E, bool D>
+void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
+    if (c) hipLaunchKernelGGL((k_paper_primary<E, D, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary<E, D, false>), grid, dim3(256), 0, st, S, P);
+}
+
+}  // namespace
+
+// Eager scenes always use D.  Each variant gets its own register allocation.
+void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const SceneView& V,
+                const StdParams& P) {
+    const DevScene S = make_scene(V);
+    if (e) {
+        if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
+        else launch_std_c<true, true, false>(c, grid, st, S, P);
+    } else if (d) {
+        if (sec) launch_std_c<false, true, true>(c, grid, st, S, P);
+        else launch_std_c<false, true, false>(c, grid, st, S, P);
+    } else {
+        if (sec) launch_std_c<false, false, true>(c, grid, st, S, P);
+        else if (c) hipLaunchKernelGGL((k_std_lean<true>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_std_lean<false>), grid, dim3(256), 0, st, S, P);
+    }
+}
+
+void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const SceneView& V, const PaperParams& P) {
+    const DevScene S = make_scene(V);
+    if (e) launch_paper_c<true, true>(c, grid, st, S, P);
+    else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
+    else if (c) hipLaunchKernelGGL((k_paper_primary_lean<true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary_lean<false>), grid, dim3(256), 0, st, S, P);
+}
+
+void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {
+    hipLaunchKernelGGL(k_paper_finish, grid, dim3(256), 0, st, P);
+}
+
+}  // namespace RT_NS

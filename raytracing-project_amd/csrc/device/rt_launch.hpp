@@ -1,0 +1,123 @@
+// rt_launch.hpp — what the host side of librtamd hands to the render kernels.
+//
+// The kernels exist twice: namespace rtd (FP64, the parity path) and
+// namespace rtf (FP32, RT_FLAG_FP32, rt_render_f32.hip).  Both are built from
+// rt_device.hpp + rt_kernels.hpp; this header holds the precision-neutral
+// launch interface: device pointers, the camera/medium in double, and the
+// per-launch parameter blocks.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt.h"
+#include "scene_compile.hpp"
+
+namespace rtamd {
+
+// Scene records in a given precision.  The double instances are
+// layout-identical to the C-ABI structs of rt.h; the float ones are the
+// converted copies the FP32 kernels read.
+template <class T>
+struct NodeR {
+    int32_t kind;
+    int32_t a, b;
+    int32_t op;
+    int32_t mat;
+    int32_t mats[5];
+    T v[24];
+    T aux[4];
+};
+template <class T>
+struct MatR {
+    T albedo[3];
+    T ambient[3];
+    T kd, ks, kr, kt;
+    T shininess;
+    T refractive_index;
+};
+template <class T>
+struct LightR {
+    T pos[3];
+    T intensity[3];
+};
+template <class T>
+struct DLightR {
+    T dir[3];
+    T radiance[3];
+};
+static_assert(sizeof(NodeR<double>) == sizeof(rt_node), "NodeR<double> must mirror rt_node");
+static_assert(sizeof(MatR<double>) == sizeof(rt_material), "MatR<double> must mirror rt_material");
+static_assert(sizeof(LightR<double>) == sizeof(rt_light), "LightR<double> must mirror rt_light");
+static_assert(sizeof(DLightR<double>) == sizeof(rt_dir_light), "DLightR<double> must mirror rt_dir_light");
+
+// Device-resident scene, precision-neutral (records are NodeR/MatR/... of
+// the launching precision).
+struct SceneView {
+    const void* nodes;
+    const void* mats;
+    const void* lights;
+    const void* dlights;
+    const DevObj* objs;
+    const DevOp* ops;
+    const float* gb;
+    int n_lights, n_dlights, n_objs;
+    int cam_nx, cam_ny;
+    int rec_limit, cull;
+    double eye[3], P[3], Lx, Ly;
+    double bg[3], amb[3], medium_index;
+};
+
+struct StdParams {
+    int W, H;
+    int n_rows;
+    const int32_t* rows;
+    const int32_t* jrow;   // jitter row of every listed row
+    const double* jit;     // 16 draws per pixel: (dx, dy) of samples 0..7
+    double* fb;
+    unsigned long long* counters;
+};
+
+struct PaperParams {
+    int W, H;
+    int n_ext;
+    int n_rows;
+    int n_list;                  // primary pass: ext indices ext_list[0..n_list) of this launch
+    const int32_t* ext_list;
+    const int32_t* ext_rows;     // rows needing a primary hit
+    const int32_t* ext_shade;    // 1 = row is rendered by this call (shade it)
+    const int32_t* nbr;          // per rendered row: ext index of r-1, r, r+1 (-1 = outside frame)
+    const int32_t* rows;         // rendered rows
+    int* hit;                    // [n_ext*W]
+    int* mat;
+    double* t;
+    double* nx;
+    double* ny;
+    double* nz;
+    double* lum;
+    double* fb;
+    unsigned long long* counters;
+};
+
+constexpr int kMaxRayStack = 8;   // transform nesting (checked on the host)
+constexpr int kMaxIvlSpill = 6;   // interval stack entries beyond the top two
+constexpr int kMaxDepth = 16;     // recursion frames (medium.recursion <= 16)
+
+constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
+constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics
+
+}  // namespace rtamd
+
+// Kernel variants (rt_kernels.hpp): E = scene has eager (transform-inside-CSG)
+// objects, D = general compact CSG (deep stacks, directional lights),
+// SEC = reflection/refraction frames, C = op counting.
+#define RT_DECLARE_LAUNCHERS(NS)                                                                                  \
+    namespace NS {                                                                                                \
+    void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,      \
+                    const rtamd::StdParams& P);                                                                   \
+    void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,               \
+                      const rtamd::PaperParams& P);                                                               \
+    void launch_paper_finish(dim3 grid, hipStream_t st, const rtamd::PaperParams& P);                             \
+    }
+RT_DECLARE_LAUNCHERS(rtd)
+RT_DECLARE_LAUNCHERS(rtf)

@@ -25,16 +25,21 @@
 #include "mt_jump.hpp"
 #include "mt_poly.hpp"
 #include "rt.h"
-#include "rt_device.hpp"
+#include "rt_launch.hpp"
 #include "rt_internal.hpp"
 #include "scene_compile.hpp"
 
-using namespace rtd;
+using rtamd::kCounterSlots;
+using rtamd::kMaxDepth;
+using rtamd::kMaxIvlSpill;
+using rtamd::kMaxRayStack;
+using rtamd::kCounterWords;
+using rtamd::PaperParams;
+using rtamd::SceneView;
+using rtamd::StdParams;
 
 namespace {
 
-constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
-constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics
 constexpr int kJitterKMax = 1024;       // twist blocks per jitter segment, upper bound
 constexpr int kJitterKMin = 64;
 
@@ -57,253 +62,6 @@ int jitter_k(int64_t words_needed) {
     return K;
 }
 
-struct StdParams {
-    int W, H;
-    int n_rows;
-    const int32_t* rows;
-    const int32_t* jrow;   // jitter row of every listed row
-    const double* jit;     // 16 draws per pixel: (dx, dy) of samples 0..7
-    double* fb;
-    unsigned long long* counters;
-};
-
-// Ray / op counters: wave reduction by shuffles, block reduction through LDS,
-// then one atomic per block and counter into one of kCounterSlots slots
-// (blockIdx-hashed).  A single hot address would serialize ~2M atomics at the
-// L2 (~6 ns each, MI355X_MICROARCH.md fan-in row) - 12 ms per 4K frame.
-template <bool C>
-__device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
-    constexpr int NW = C ? 18 : 2;
-    __shared__ unsigned long long red[4][NW];
-    unsigned long long v[NW];
-    v[0] = ni;
-    v[1] = no;
-    if constexpr (C) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[2 + k] = cnt.c[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NW; ++k)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < NW; ++k) red[wave][k] = v[k];
-    __syncthreads();
-    if (threadIdx.x < NW) {
-        const unsigned long long sum = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                       red[3][threadIdx.x];
-        const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x) % kCounterSlots;
-        if (sum) atomicAdd(&ctr[(size_t)slot * kCounterWords + threadIdx.x], sum);
-    }
-}
-
-// Occupancy target of the lean variants (E = D = SEC = false): 4 waves/SIMD
-// caps them at 128 VGPRs; the few values the compiler then spills are
-// long-lived (stored once, reloaded once), and the extra wave per SIMD hides
-// FP64 latency (measured 21.6 -> 19.2 ms on config 4; 5 and 6 are slower).
-#ifndef RT_LEAN_WAVES
-#define RT_LEAN_WAVES 4
-#endif
-
-template <bool E, bool D, bool SEC, bool C, bool DL = true>
-__device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int s = lane & 7;
-    const int pix = lane >> 3;
-    const int x = blockIdx.x * 8 + (wave & 1) * 4 + (pix & 3);
-    const int ri = blockIdx.y * 4 + (wave >> 1) * 2 + (pix >> 2);
-    const bool active = x < P.W && ri < P.n_rows;
-    uint32_t ni = 0, no = 0;
-    Cnt<C> cnt;
-    V3 c = v3(0.0, 0.0, 0.0);
-    if (active) {
-        const int r = P.rows[ri];
-        const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
-        // draws 16p+2s, 16p+2s+1 of the stream: dx, dy (tracer.cpp:293)
-        const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)P.jrow[ri] * P.W + x) * 16 + 2 * s);
-        const DRay ray = gen_ray_subpixel(S, x, y, j.x, j.y);
-        c = trace<E, D, SEC, DL>(S, ray, ni, no, cnt);
-    }
-    // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
-    const int base = lane & ~7;
-    V3 acc = v3(0.0, 0.0, 0.0);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const double cx = __shfl(c.x, base + k);
-        const double cy = __shfl(c.y, base + k);
-        const double cz = __shfl(c.z, base + k);
-        acc.x += cx;
-        acc.y += cy;
-        acc.z += cz;
-    }
-    if (active && s == 0) {
-        const double inv = 1.0 / (double)8;
-        double* o = P.fb + ((size_t)ri * P.W + x) * 3;
-        o[0] = acc.x * inv;
-        o[1] = acc.y * inv;
-        o[2] = acc.z * inv;
-    }
-    flush_counters(P.counters, ni, no, cnt);
-}
-
-template <bool E, bool D, bool SEC, bool C>
-__global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
-    std_body<E, D, SEC, C>(S, P);
-}
-
-template <bool C>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
-                                                                                                       StdParams P) {
-    std_body<false, false, false, C, false>(S, P);
-}
-
-struct PaperParams {
-    int W, H;
-    int n_ext;
-    int n_rows;
-    int n_list;                  // primary pass: ext indices ext_list[0..n_list) of this launch
-    const int32_t* ext_list;
-    const int32_t* ext_rows;     // rows needing a primary hit
-    const int32_t* ext_shade;    // 1 = row is rendered by this call (shade it)
-    const int32_t* nbr;          // per rendered row: ext index of r-1, r, r+1 (-1 = outside frame)
-    const int32_t* rows;         // rendered rows
-    int* hit;                    // [n_ext*W]
-    int* mat;
-    double* t;
-    double* nx;
-    double* ny;
-    double* nz;
-    double* lum;
-    double* fb;
-    unsigned long long* counters;
-};
-
-template <bool E, bool D, bool C, bool DL = true>
-__device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
-    // block 16x16 pixels, wave 8x8
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = x < P.W && li < P.n_list;
-    uint32_t ni = 0, no = 0;
-    Cnt<C> cnt;
-    if (active) {
-        const int ei = P.ext_list[li];
-        const int y = P.ext_rows[ei];
-        const DRay r = gen_ray(S, x, y);
-        double ht = 0.0;
-        DHit h;
-        ++ni;
-        const bool hits = scene_intersect<E, D>(S, r, 1e-4, RT_INF, ht, h, cnt);
-        const size_t idx = (size_t)ei * P.W + x;
-        P.hit[idx] = hits ? 1 : 0;
-        P.t[idx] = ht;
-        P.nx[idx] = h.n.x;
-        P.ny[idx] = h.n.y;
-        P.nz[idx] = h.n.z;
-        P.mat[idx] = hits ? h.mat : -3;
-        if (P.ext_shade[ei]) {
-            // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
-            V3 base = v3(1.0, 1.0, 1.0);
-            if (hits) base = shade<E, D, DL>(S, ht, h, normalized(vneg(r.d)), no, cnt);
-            P.lum[idx] = 0.299 * base.x + 0.587 * base.y + 0.114 * base.z;
-        }
-    }
-    flush_counters(P.counters, ni, no, cnt);
-}
-
-template <bool E, bool D, bool C>
-__global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
-    paper_primary_body<E, D, C>(S, P);
-}
-
-template <bool C>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
-    DevScene S, PaperParams P) {
-    paper_primary_body<false, false, C, false>(S, P);
-}
-
-// apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
-__device__ __forceinline__ double crosshatch(double lum, int x, int y) {
-    if (lum < 0.15) return 0.0;
-    const double darkness = 1.0 - lum;
-    const bool diag1 = ((x + y) % 4) < 1;
-    const bool diag2 = ((x - y) % 4) < 1;
-    const bool horizontal = (y % 4) < 1;
-    bool draw = false;
-    if (darkness > 0.8) draw = (diag1 && diag2) || horizontal;
-    else if (darkness > 0.65) draw = (diag1 && diag2) || (horizontal && ((x + y) % 3 == 0));
-    else if (darkness > 0.5) draw = (diag1 && diag2) || (horizontal && ((x + y) % 4 == 0));
-    else if (darkness > 0.35) draw = diag1 || (horizontal && ((x + y) % 3 == 0));
-    else if (darkness > 0.2) draw = diag1;
-    else if (darkness > 0.12) draw = diag1 && ((x + y) % 8) < 2;
-    return draw ? 0.0 : 1.0;
-}
-
-__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= P.W || ri >= P.n_rows) return;
-    const int y = P.rows[ri];
-    const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
-    const size_t ci = (size_t)e_c * P.W + x;
-    const bool ch = P.hit[ci] != 0;
-    const double ct = P.t[ci];
-    const V3 cn = v3(P.nx[ci], P.ny[ci], P.nz[ci]);
-    const int cm = P.mat[ci];
-    // get_edge_strength (tracer.cpp:133-178): neighbours (-1,0) (1,0) (0,-1) (0,1)
-    double maxEdge = 0.0;
-    int valid = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int dx = (i == 0) ? -1 : (i == 1) ? 1 : 0;
-        const int dy = (i == 2) ? -1 : (i == 3) ? 1 : 0;
-        const int nxp = x + dx, nyp = y + dy;
-        if (nxp < 0 || nxp >= P.W || nyp < 0 || nyp >= P.H) continue;
-        ++valid;
-        const int er = (dy < 0) ? e_up : (dy > 0) ? e_dn : e_c;
-        const size_t ni = (size_t)er * P.W + nxp;
-        const bool nh = P.hit[ni] != 0;
-        if (ch != nh) {
-            maxEdge = dmax(maxEdge, 0.9);
-            continue;
-        }
-        if (ch && nh) {
-            const double nt = P.t[ni];
-            const double minD = dmin(ct, nt), maxD = dmax(ct, nt);
-            if (minD > 1e-4 && maxD / minD > 3.0) maxEdge = dmax(maxEdge, 0.6);
-            const double nd = dot3(cn, v3(P.nx[ni], P.ny[ni], P.nz[ni]));
-            if (nd < 0.2) maxEdge = dmax(maxEdge, 0.5);
-            if (cm != P.mat[ni] && nd < 0.7) maxEdge = dmax(maxEdge, 0.3);
-        }
-    }
-    if (valid < 4) maxEdge *= 0.5;
-    const double edge = maxEdge;
-    V3 o;
-    if (edge > 0.8) {
-        o = v3(0.0, 0.0, 0.0);
-    } else if (edge > 0.5) {
-        o = v3(0.2, 0.2, 0.2);
-    } else {
-        const double h = crosshatch(P.lum[ci], x, y);
-        o = v3(h, h, h);
-        if (edge > 0.3) {
-            const double darken = (edge - 0.3) * 0.4;
-            o.x *= (1.0 - darken);
-            o.y *= (1.0 - darken);
-            o.z *= (1.0 - darken);
-        }
-    }
-    double* dst = P.fb + ((size_t)ri * P.W + x) * 3;
-    dst[0] = o.x;
-    dst[1] = o.y;
-    dst[2] = o.z;
-}
-
 __global__ void k_scatter_rows(const double* __restrict__ src, const int32_t* __restrict__ rows, int n_rows, int W,
                                double* __restrict__ dst) {
     const size_t row_len = (size_t)W * 3;
@@ -322,40 +80,6 @@ __global__ void k_to_rgb8(const double* __restrict__ fb, size_t n, uint8_t* __re
         c = (0.0 < c) ? c : 0.0;          // std::max(0.0, .)
         out[i] = (uint8_t)(int)round(c * 255.0);   // round half away from zero (core.h:316)
     }
-}
-
-// Kernel variants: E = scene has eager (transform-inside-CSG) objects,
-// D = some compact CSG needs an interval stack deeper than 2 (not a left-deep
-// fold), SEC = reflection/refraction frames needed, C = op counting.  Eager
-// scenes always use D.  Each variant gets its own register allocation.
-template <bool E, bool D, bool SEC>
-void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std<E, D, SEC, false>), grid, dim3(256), 0, st, S, P);
-}
-void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (e) {
-        if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
-        else launch_std_c<true, true, false>(c, grid, st, S, P);
-    } else if (d) {
-        if (sec) launch_std_c<false, true, true>(c, grid, st, S, P);
-        else launch_std_c<false, true, false>(c, grid, st, S, P);
-    } else {
-        if (sec) launch_std_c<false, false, true>(c, grid, st, S, P);
-        else if (c) hipLaunchKernelGGL((k_std_lean<true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_std_lean<false>), grid, dim3(256), 0, st, S, P);
-    }
-}
-template <bool E, bool D>
-void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
-    if (c) hipLaunchKernelGGL((k_paper_primary<E, D, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_paper_primary<E, D, false>), grid, dim3(256), 0, st, S, P);
-}
-void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
-    if (e) launch_paper_c<true, true>(c, grid, st, S, P);
-    else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
-    else if (c) hipLaunchKernelGGL((k_paper_primary_lean<true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_paper_primary_lean<false>), grid, dim3(256), 0, st, S, P);
 }
 
 // ------------------------------------------------------------ host side
@@ -390,6 +114,7 @@ struct DBuf {
 struct Workspace {
     std::mutex mu;
     DBuf nodes, mats, lights, dlights, objs, ops, gb;
+    DBuf nodes_f, mats_f, lights_f, dlights_f;   // float copies (RT_FLAG_FP32)
     DBuf rows, jit, ckpt, jscratch, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
     std::map<int, rtamd::JitterPlan> jplan;   // per segment length K
@@ -426,9 +151,9 @@ struct rt_frame {
     Workspace* ws = nullptr;
     std::unique_lock<std::mutex> lock;
     hipStream_t st = nullptr;
-    DevScene S;
+    SceneView S;
     int W = 0, H = 0, mode = 0, n_rows = 0;
-    bool eager = false, deep = false, secondary = false, count_ops = false;
+    bool eager = false, deep = false, secondary = false, count_ops = false, fp32 = false;
     bool traced = false;
     std::vector<int32_t> rows;
     std::vector<int32_t> rows_jrow;            // standard mode: rows | jitter row of each
@@ -447,9 +172,58 @@ struct rt_frame {
     std::vector<rt_material> mats;
     std::vector<rt_light> lights;
     std::vector<rt_dir_light> dlights;
+    std::vector<rtamd::NodeR<float>> nodes_f;
+    std::vector<rtamd::MatR<float>> mats_f;
+    std::vector<rtamd::LightR<float>> lights_f;
+    std::vector<rtamd::DLightR<float>> dlights_f;
 };
 
 namespace {
+
+template <size_t N>
+void to_float(float (&dst)[N], const double (&src)[N]) {
+    for (size_t i = 0; i < N; ++i) dst[i] = (float)src[i];
+}
+
+// Float copies of the scene records for the FP32 kernels (RT_FLAG_FP32).
+void make_float_scene(rt_frame& f) {
+    f.nodes_f.resize(f.nodes.size());
+    for (size_t i = 0; i < f.nodes.size(); ++i) {
+        const rt_node& s = f.nodes[i];
+        rtamd::NodeR<float>& o = f.nodes_f[i];
+        o.kind = s.kind;
+        o.a = s.a;
+        o.b = s.b;
+        o.op = s.op;
+        o.mat = s.mat;
+        for (int k = 0; k < 5; ++k) o.mats[k] = s.mats[k];
+        to_float(o.v, s.v);
+        to_float(o.aux, s.aux);
+    }
+    f.mats_f.resize(f.mats.size());
+    for (size_t i = 0; i < f.mats.size(); ++i) {
+        const rt_material& s = f.mats[i];
+        rtamd::MatR<float>& o = f.mats_f[i];
+        to_float(o.albedo, s.albedo);
+        to_float(o.ambient, s.ambient);
+        o.kd = (float)s.kd;
+        o.ks = (float)s.ks;
+        o.kr = (float)s.kr;
+        o.kt = (float)s.kt;
+        o.shininess = (float)s.shininess;
+        o.refractive_index = (float)s.refractive_index;
+    }
+    f.lights_f.resize(f.lights.size());
+    for (size_t i = 0; i < f.lights.size(); ++i) {
+        to_float(f.lights_f[i].pos, f.lights[i].pos);
+        to_float(f.lights_f[i].intensity, f.lights[i].intensity);
+    }
+    f.dlights_f.resize(f.dlights.size());
+    for (size_t i = 0; i < f.dlights.size(); ++i) {
+        to_float(f.dlights_f[i].dir, f.dlights[i].dir);
+        to_float(f.dlights_f[i].radiance, f.dlights[i].radiance);
+    }
+}
 
 int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
                 hipStream_t st, rt_frame** out) {
@@ -509,6 +283,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->deep = cs.max_ivl_depth > 2 || d.n_dir_lights > 0;
     f->secondary = secondary;
     f->count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
+    f->fp32 = (flags & RT_FLAG_FP32) != 0;
     f->rows.assign(rows_host, rows_host + n_rows);
     f->t_start = t_start;
     if (!ws.ev[0])
@@ -520,10 +295,18 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->lights.assign(d.lights, d.lights + d.n_lights);
     f->dlights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
     f->cs = std::move(cs);
-    HIP_TRY(upload(ws.nodes, f->nodes, st));
-    HIP_TRY(upload(ws.mats, f->mats, st));
-    HIP_TRY(upload(ws.lights, f->lights, st));
-    HIP_TRY(upload(ws.dlights, f->dlights, st));
+    if (f->fp32) {
+        make_float_scene(*f);
+        HIP_TRY(upload(ws.nodes_f, f->nodes_f, st));
+        HIP_TRY(upload(ws.mats_f, f->mats_f, st));
+        HIP_TRY(upload(ws.lights_f, f->lights_f, st));
+        HIP_TRY(upload(ws.dlights_f, f->dlights_f, st));
+    } else {
+        HIP_TRY(upload(ws.nodes, f->nodes, st));
+        HIP_TRY(upload(ws.mats, f->mats, st));
+        HIP_TRY(upload(ws.lights, f->lights, st));
+        HIP_TRY(upload(ws.dlights, f->dlights, st));
+    }
     HIP_TRY(upload(ws.objs, f->cs.objs, st));
     HIP_TRY(upload(ws.ops, f->cs.ops, st));
     HIP_TRY(upload(ws.gb, f->cs.gbounds, st));
@@ -531,14 +314,14 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
 
-    DevScene& S = f->S;
-    S.nodes = ws.nodes.as<rt_node>();
-    S.mats = ws.mats.as<rt_material>();
-    S.lights = ws.lights.as<rt_light>();
-    S.dlights = ws.dlights.as<rt_dir_light>();
+    SceneView& S = f->S;
+    S.nodes = f->fp32 ? ws.nodes_f.p : ws.nodes.p;
+    S.mats = f->fp32 ? ws.mats_f.p : ws.mats.p;
+    S.lights = f->fp32 ? ws.lights_f.p : ws.lights.p;
+    S.dlights = f->fp32 ? ws.dlights_f.p : ws.dlights.p;
     S.n_dlights = d.n_dir_lights;
-    S.objs = ws.objs.as<DevObj>();
-    S.ops = ws.ops.as<DevOp>();
+    S.objs = ws.objs.as<rtamd::DevObj>();
+    S.ops = ws.ops.as<rtamd::DevOp>();
     S.gb = ws.gb.as<float>();
     S.n_lights = d.n_lights;
     S.n_objs = (int)f->cs.objs.size();
@@ -669,7 +452,8 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         P.fb = fb;
         P.counters = ctr;
         dim3 grid((W + 7) / 8, (n + 3) / 4);
-        launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
+        if (f->fp32) rtf::launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
+        else rtd::launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
         HIP_TRY(hipGetLastError());
     } else {
         // primary hits of the ext rows this chunk reads that no earlier chunk computed
@@ -716,11 +500,13 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
             const std::vector<int32_t>& L = f->stage.back();
             HIP_TRY(hipMemcpyAsync(d_list, L.data(), L.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
             dim3 g1((W + 15) / 16, (P.n_list + 15) / 16);
-            launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
+            if (f->fp32) rtf::launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
+            else rtd::launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
             HIP_TRY(hipGetLastError());
         }
         dim3 g2((W + 63) / 64, (n + 3) / 4);
-        hipLaunchKernelGGL(k_paper_finish, g2, dim3(256), 0, st, P);
+        if (f->fp32) rtf::launch_paper_finish(g2, st, P);
+        else rtd::launch_paper_finish(g2, st, P);
         HIP_TRY(hipGetLastError());
     }
     if ((int)ws.tev.size() <= f->n_tev) {

@@ -38,6 +38,7 @@ RT_ERR_NO_DEVICE = -7
 RT_FLAG_NONE = 0
 RT_FLAG_COUNT_OPS = 1
 RT_FLAG_NO_CULL = 2
+RT_FLAG_FP32 = 4   # non-parity FP32 fast path
 
 NODE_SPHERE, NODE_HALFSPACE, NODE_POKEBALL, NODE_TRANSLATION, NODE_SCALING, NODE_ROTATION, NODE_CSG = range(7)
 CSG_UNION, CSG_INTERSECTION, CSG_DIFFERENCE = range(3)

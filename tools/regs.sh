@@ -1,10 +1,13 @@
 #!/bin/bash
-# Print VGPRs / scratch / occupancy of every kernel in rt_render.hip (host-side, no GPU).
-# Usage: tools/regs.sh [extra hipcc flags]
+# Print VGPRs / scratch / occupancy of every render kernel, both precisions
+# (host-side, no GPU).  Usage: tools/regs.sh [extra hipcc flags]
 cd "$(dirname "$0")/../raytracing-project_amd" || exit 1
-/opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
-  -munsafe-fp-atomics -I../include -Icsrc/host -Icsrc/device "$@" -c csrc/device/rt_render.hip -o /tmp/regs_probe.o \
-  -Rpass-analysis=kernel-resource-usage 2>&1 |
-  awk '/Function Name:/ {n=$(NF-1); sub(/.*_GLOBAL__N_1[0-9]+/, "", n); sub(/EvN3rtd.*/, "", n)}
-       /VGPRs:/ {v=$(NF-1)} /ScratchSize/ {sc=$(NF-1)}
-       /Occupancy/ {printf "%-32s vgpr %4s scratch %5s occ %s\n", n, v, sc, $(NF-1)}'
+for src in rt_kernels_f64 rt_kernels_f32; do
+  echo "== $src"
+  /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+    -munsafe-fp-atomics -I../include -Icsrc/host -Icsrc/device "$@" -c csrc/device/$src.hip -o /tmp/regs_probe.o \
+    -Rpass-analysis=kernel-resource-usage 2>&1 |
+    awk '/Function Name:/ {n=$(NF-1); sub(/.*_GLOBAL__N_1[0-9]+/, "", n); sub(/EvN3rt[df].*/, "", n)}
+         /VGPRs:/ {v=$(NF-1)} /ScratchSize/ {sc=$(NF-1)}
+         /Occupancy/ {printf "%-32s vgpr %4s scratch %5s occ %s\n", n, v, sc, $(NF-1)}'
+done
