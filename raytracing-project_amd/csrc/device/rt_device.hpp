@@ -1,7 +1,7 @@
 // rt_device.hpp — FP64 device restatement of the reference trace path for
 // gfx950 (CDNA4).  Operation order follows the reference step for step and
 // the file is compiled with -ffp-contract=off and IEEE div/sqrt, so every
-// rounding matches the x86-64 reference except pow()/acos(), which come from
+// rounding matches the x86-64 reference except pow() (non-integer exponents)/acos(), which come from
 // the device math library (<= 1 ulp apart).  Citations are
 // raytracer/src/<file>:<line> of the reference.
 //
@@ -706,6 +706,41 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
         }
         return;
     }
+    if (op == RT_CSG_UNION) {
+        // Closed form of the union sweep when no comparison of the sort can
+        // tie: four finite events, every pair farther apart than the
+        // comparator's 1e-6 (so event_less is plain '<' and the sorted order
+        // is the numeric one) and each interval ordered (t0 < t1).  Then the
+        // first event is the earlier entry X; the result is X, extended to
+        // the other interval Y's exit when Y enters before X exits - or, when
+        // the origin lies inside A or B, the same from t = 0 with the
+        // inside-at-origin entry (csg.cpp:98-152).  Other lanes take the
+        // general sweep below.
+        const real e = RV(1e-6);
+        const bool easy = __builtin_isfinite(A.t0) && __builtin_isfinite(A.t1) && __builtin_isfinite(B.t0) &&
+                          __builtin_isfinite(B.t1) && (A.t1 - A.t0 > e) && (B.t1 - B.t0 > e) &&
+                          (fabs_r(A.t0 - B.t0) > e) && (fabs_r(A.t0 - B.t1) > e) && (fabs_r(A.t1 - B.t0) > e) &&
+                          (fabs_r(A.t1 - B.t1) > e);
+        if (easy) {
+            const bool inA = (A.t0 < e) && (A.t1 > e);
+            const bool inB = (B.t0 < e) && (B.t1 > e);
+            const bool xa = inA || (!inB && A.t0 < B.t0);
+            const real x1 = xa ? A.t1 : B.t1;
+            const real y0 = xa ? B.t0 : A.t0;
+            const real y1 = xa ? B.t1 : A.t1;
+            const bool ext_y = (y0 < x1) && (y1 > x1);
+            const bool org = inA || inB;
+            const int xc0 = xa ? A.c0 : B.c0;
+            R.ok = 1;
+            R.t0 = org ? RV(0.0) : (xa ? A.t0 : B.t0);
+            R.s0 = xa ? A.s0 : B.s0;
+            R.c0 = org ? ((xc0 & ~REF_FLIP) | REF_ORIGIN) : xc0;
+            R.t1 = ext_y ? y1 : x1;
+            R.s1 = (ext_y != xa) ? A.s1 : B.s1;
+            R.c1 = (ext_y != xa) ? A.c1 : B.c1;
+            return;
+        }
+    }
     // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
     real et[4];
     int ec[4];
@@ -1129,6 +1164,38 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
 }
 
 // ----------------------------------------------------------------- shading
+// std::pow(x, shininess) of the specular term (shading.cpp:120).  The
+// reference's glibc pow is correctly rounded in practice; the device
+// library's pow is not always, and costs ~10 % of a frame.  Every shininess
+// in the reference's scenes is a small integer, so for integer exponents
+// 0..1023 x^k is evaluated by left-to-right binary powering in double-double
+// arithmetic (exact products by fma, ~2^-100 relative error), and rounded
+// once: the correctly rounded x^k.  Other exponents use the library pow.
+__device__ __forceinline__ double pow_spec(double x, double y) {
+    const int k = (int)y;
+    if (!(y >= 0.0 && y < 1024.0 && (double)k == y)) return pow(x, y);
+    if (k == 0) return 1.0;   // pow(x, 0) = 1 for every x
+    const int top = 31 - __builtin_clz(k);
+    double h = x, l = 0.0;
+    for (int i = top - 1; i >= 0; --i) {
+        // (h, l)^2
+        double p = h * h;
+        double e = __builtin_fma(h, h, -p);
+        e = e + (2.0 * h) * l;
+        h = p + e;
+        l = e - (h - p);
+        if ((k >> i) & 1) {   // (h, l) * x
+            p = h * x;
+            e = __builtin_fma(h, x, -p);
+            e = e + l * x;
+            h = p + e;
+            l = e - (h - p);
+        }
+    }
+    return h + l;
+}
+__device__ __forceinline__ float pow_spec(float x, float y) { return pow(x, y); }
+
 __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
     return v3(RV(1.0) - (RV(1.0) - a.x) * (RV(1.0) - b.x), RV(1.0) - (RV(1.0) - a.y) * (RV(1.0) - b.y), RV(1.0) - (RV(1.0) - a.z) * (RV(1.0) - b.z));
 }
@@ -1175,7 +1242,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             const V3 rr = normalized(v3(RV(2.0) * dot3(n, wi) * n.x - wi.x, RV(2.0) * dot3(n, wi) * n.y - wi.y,
                                         RV(2.0) * dot3(n, wi) * n.z - wi.z));
             const real rdotv = dmax(RV(0.0), dot3(rr, wo));
-            const real spec = pow(rdotv, m->shininess) * m->ks;
+            const real spec = pow_spec(rdotv, m->shininess) * m->ks;
             Es = v3(L->radiance[0] * spec, L->radiance[1] * spec, L->radiance[2] * spec);
         }
         E = combine(E, combine(Ed, Es));
@@ -1227,7 +1294,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 const V3 rr = normalized(v3(RV(2.0) * dot3(n, wi) * n.x - wi.x, RV(2.0) * dot3(n, wi) * n.y - wi.y,
                                             RV(2.0) * dot3(n, wi) * n.z - wi.z));
                 const real rdotv = dmax(RV(0.0), dot3(rr, wo));
-                const real spec = pow(rdotv, shin) * ks;
+                const real spec = pow_spec(rdotv, shin) * ks;
                 Es = v3(IL.x * spec, IL.y * spec, IL.z * spec);
             }
             E = combine(E, combine(Ed, Es));

@@ -48,6 +48,26 @@ def test_render_matches_oracle(gpu, name, mode):
         assert np.array_equal(fb, ref), "paper mode must be bit-exact"
 
 
+# Mid-resolution frames: more rays through the CSG fast paths and group culls
+# (320x180 and up; the oracle runs them in ~1 s on the box's cores).
+MID = {
+    "cfg4_320": lambda: scenes.config_json(4, dpi=80)[0],
+    "cfg3_320": lambda: scenes.config_json(3, dpi=80)[0],
+    "snorlax_320": lambda: json.dumps(scenes.with_dpi(scenes.load_example("snorlax"), 80)),
+    "csg_ops_240": lambda: json.dumps(scenes.torture_scenes(dpi=60)["csg_ops"]),
+    "csg_groups_240": lambda: json.dumps(scenes.torture_scenes(dpi=60)["csg_groups"]),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(MID))
+def test_midres_matches_oracle(gpu, name):
+    fb, ref, st, ost = _compare(gpu, MID[name](), 0)
+    assert np.abs(fb - ref).max() <= TOL
+    assert st.rays_intersect == ost.rays_intersect
+    assert st.rays_occluded == ost.rays_occluded
+
+
 @pytest.mark.gpu
 def test_no_cull_flag_same_image(gpu):
     text = SMALL["snorlax"]()
