@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rt.h"
 #include "rt_launch.hpp"
 #include "scene_compile.hpp"
@@ -131,6 +133,7 @@ struct DevScene {
     const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
     int n_lights, n_objs;
     int n_dlights;
+    int n_bounded;   // objects with a bounding ball (wave-level culling pays only when > 0)
     int cam_nx, cam_ny;
     int rec_limit, cull;
     real eye[3], P[3], Lx, Ly;
@@ -1163,6 +1166,124 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
     return hit;
 }
 
+
+// ------------------------------------------- wave-level shadow-ray culling
+// A shadow query of a whole wave (every lane active; lanes that need no
+// query pass need = false) is culled object by object in ONE transposed
+// test instead of one wave-uniform ball test per object: the segments
+// [o + tmin d, o + tmax d] of all querying lanes lie inside the capsule of
+// radius rho around [C0, C1], C0 / C1 the first querying lane's endpoints
+// and rho the largest distance of any lane's endpoint from them (a point
+// (1-s) A_i + s B_i is within (1-s)|A_i - C0| + s|B_i - C1| of the axis).
+// Lane j then tests object j's bounding ball against that capsule, and one
+// ballot gives the objects any lane can reach.  Like ball_touch the test is
+// conservative in f32 (a margin of 1e-5 of every magnitude involved), so it
+// never drops an object some lane's segment touches: results are unchanged.
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {   // every lane must be active
+    // row_ror:1,2,4,8 (DPP) leaves each row's maximum in all its lanes
+    v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false));
+    v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false));
+    v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false));
+    v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return umax32(umax32(r0, r1), umax32(r2, r3));
+}
+
+__device__ __forceinline__ float rdlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ bool capsule_touch(const float* g, float ax, float ay, float az, float ux, float uy,
+                                              float uz, float uu, float rho, float mag) {
+    const float wx = g[0] - ax, wy = g[1] - ay, wz = g[2] - az;
+    const float wu = __builtin_fmaf(wx, ux, __builtin_fmaf(wy, uy, wz * uz));
+    const float s = uu > 0.0f ? __builtin_amdgcn_fmed3f(wu * __builtin_amdgcn_rcpf(uu), 0.0f, 1.0f) : 0.0f;
+    const float qx = __builtin_fmaf(-s, ux, wx), qy = __builtin_fmaf(-s, uy, wy), qz = __builtin_fmaf(-s, uz, wz);
+    const float d2 = __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz));
+    const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
+    const float R = g[3] + rho + m;
+    return !(d2 > R * R);   // NaN passes
+}
+
+template <class CT>
+__device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
+    for (int i = 0; i < n; ++i) cnt.inc(k);
+}
+
+// Scene::occluded for the querying lanes of a fully active wave.  Returns
+// false for lanes with need = false.
+template <bool EAGER, bool DEEP, class CT>
+__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, CT& cnt) {
+    const FRay fr = to_fray(r);
+    const float ftmin = (float)tmin, ftmax = (float)tmax;
+    const float Ax = __builtin_fmaf(ftmin, fr.dx, fr.ox), Ay = __builtin_fmaf(ftmin, fr.dy, fr.oy),
+                Az = __builtin_fmaf(ftmin, fr.dz, fr.oz);
+    const float Bx = __builtin_fmaf(ftmax, fr.dx, fr.ox), By = __builtin_fmaf(ftmax, fr.dy, fr.oy),
+                Bz = __builtin_fmaf(ftmax, fr.dz, fr.oz);
+    const bool fin = __builtin_isfinite(Ax + Ay + Az + Bx + By + Bz);
+    const uint64_t nm = __ballot(need);
+    if (!nm) return false;
+    if (__any(need && !fin)) {   // unbounded or non-finite segments: the per-object loop
+        bool hit = false;
+        if (need) hit = scene_occluded<EAGER, DEEP>(S, r, tmin, tmax, cnt);
+        return hit;
+    }
+    const int f = __builtin_ctzll(nm);
+    const float ax = rdlane_f(Ax, f), ay = rdlane_f(Ay, f), az = rdlane_f(Az, f);
+    const float bx = rdlane_f(Bx, f), by = rdlane_f(By, f), bz = rdlane_f(Bz, f);
+    float da = (Ax - ax) * (Ax - ax) + (Ay - ay) * (Ay - ay) + (Az - az) * (Az - az);
+    float db = (Bx - bx) * (Bx - bx) + (By - by) * (By - by) + (Bz - bz) * (Bz - bz);
+    const float d = need ? __builtin_fmaxf(da, db) : 0.0f;
+    const float rho = __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(d))));
+    const float ux = bx - ax, uy = by - ay, uz = bz - az;
+    const float uu = __builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz));
+    const float mag = __builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
+                      __builtin_fabsf(by) + __builtin_fabsf(bz) + rho + 1.0f;
+    const int lane = __lane_id();
+    bool hit = false;
+    for (int base = 0; base < S.n_objs; base += 64) {
+        const int j = base + lane;
+        bool pass = false;
+        if (j < S.n_objs) {
+            const DevObj& ob = S.objs[j];
+            pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
+                   (!ob.has_bound || capsule_touch(ob.fb, ax, ay, az, ux, uy, uz, uu, rho, mag));
+        }
+        uint64_t m = __ballot(pass);
+        if constexpr (!std::is_same<CT, Cnt<false>>::value) {
+            if (need) {
+                int skipped = 0;
+                for (int o = base; o < S.n_objs && o < base + 64; ++o) {
+                    const int k = S.objs[o].kind;
+                    if (k != rtamd::OBJ_GROUP && k != rtamd::OBJ_NEVER && !((m >> (o - base)) & 1)) ++skipped;
+                }
+                cnt_add(cnt, RT_OPC_CULLED, skipped);
+            }
+        }
+        while (m) {
+            const int o = base + __builtin_ctzll(m);
+            m &= m - 1;
+            const DevObj ob = S.objs[o];
+            if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound) {   // expensive objects: per-lane segment test
+                if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
+                    if (need) cnt.inc(RT_OPC_CULLED);
+                    continue;
+                }
+            }
+            if (need && !hit) {
+                real t = RV(0.0), ts = RV(0.0);
+                V3 p;
+                int code = 0;
+                hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
+            }
+            if (__all(hit || !need)) return hit;
+        }
+    }
+    return hit;
+}
+
 // ----------------------------------------------------------------- shading
 // std::pow(x, shininess) of the specular term (shading.cpp:120).  The
 // reference's glibc pow is correctly rounded in practice; the device
@@ -1205,9 +1326,17 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 // DL: the scene may have directional lights (the lean kernels, chosen only
 // for scenes without, do not carry their code or registers).
 template <bool EAGER, bool DEEP, bool DL, class CT>
-__device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt) {
-    if (hit.mat < 0) return v3(RV(1.0), RV(0.0), RV(1.0));
-    cnt.inc(RT_OPC_SHADE_CALL);
+__device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt,
+                    bool valid = true) {
+    // valid = false: a lane of the wave that has nothing to shade (a primary
+    // miss) but keeps the wave fully active for scene_occluded_wave; its
+    // result is discarded by the caller.
+    const bool has_mat = hit.mat >= 0;
+    valid = valid && has_mat;
+    if (valid) cnt.inc(RT_OPC_SHADE_CALL);
+    // full-wave shadow queries (scene_occluded_wave) need every lane active
+    // (with fewer than 4 bounded objects the per-object wave tests are cheaper)
+    const bool wave_full = S.cull && S.n_bounded >= 4 && __builtin_amdgcn_read_exec() == ~0ull;
     const V3 n = hit.n;
     const real eps = dmax(RV(1e-3), RV(1e-4) * ht);
     // Two passes over the lights so that only (p, n, eps) stay live across
@@ -1218,11 +1347,12 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
     // further rounds of the same two passes.
     V3 E = v3(RV(0.0), RV(0.0), RV(0.0));
     {
-        const MatT* m = &S.mats[hit.mat];
+        const MatT* m = &S.mats[valid ? hit.mat : 0];
         E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
     }
     // directional lights first (shading.cpp:45-76): no falloff, shadow ray to infinity
     for (int li = 0; DL && li < S.n_dlights; ++li) {
+        if (!valid) break;
         const DLightT* L = &S.dlights[li];
         cnt.inc(RT_OPC_LIGHT_EVAL);
         const V3 wi = normalized(v3(-L->dir[0], -L->dir[1], -L->dir[2]));
@@ -1247,26 +1377,35 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
         }
         E = combine(E, combine(Ed, Es));
     }
-    for (int l0 = 0; l0 < S.n_lights; l0 += 32) {
+    for (int l0 = 0; __any(valid) && l0 < S.n_lights; l0 += 32) {
         const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
         uint32_t lit = 0;
         for (int li = l0; li < l1; ++li) {
             const LightT* L = &S.lights[li];
-            cnt.inc(RT_OPC_LIGHT_EVAL);
+            if (valid) cnt.inc(RT_OPC_LIGHT_EVAL);
             V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
             real d2 = dot3(tl, tl);
             if (d2 <= RV(0.01)) d2 = RV(0.01);
             const real dist = sqrt_r(d2);
             const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
             const real ndotl = dmax(RV(0.0), dot3(n, wi));
-            if (ndotl <= RV(0.0)) continue;
             const real max_t = dist - eps;
-            if (max_t <= eps) continue;
+            // shading.cpp:86-103: back-facing lights and lights closer than
+            // the shadow epsilon are skipped before the occlusion query
+            const bool need = valid && ndotl > RV(0.0) && max_t > eps;
+            if (!__any(need)) continue;
             const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
             const DRay sr = make_ray(so, wi);
-            ++n_occl;
-            if (scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt)) continue;
-            lit |= 1u << (li - l0);
+            bool occ = false;
+            if (wave_full) {
+                occ = scene_occluded_wave<EAGER, DEEP>(S, sr, eps, max_t, need, cnt);
+            } else if (need) {
+                occ = scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt);
+            }
+            if (need) {
+                ++n_occl;
+                if (!occ) lit |= 1u << (li - l0);
+            }
         }
         if (!lit) continue;
         const MatT* m = &S.mats[hit.mat];
@@ -1303,7 +1442,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
     E.x = dmin(RV(1.5), E.x);
     E.y = dmin(RV(1.5), E.y);
     E.z = dmin(RV(1.5), E.z);
-    return E;
+    return has_mat ? E : v3(RV(1.0), RV(0.0), RV(1.0));   // magenta for a null material (shading.cpp:33)
 }
 
 // ---------------------------------------------------------------- tracing
@@ -1324,9 +1463,14 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         if (S.rec_limit <= 0) return v3(RV(0.0), RV(0.0), RV(0.0));
         real ht = RV(0.0);
         DHit h;
+        h.mat = -1;
         ++n_isect;
-        if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
-        return shade<EAGER, DEEP, DL>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
+        // miss lanes stay in shade() (valid = false) so that the wave stays
+        // fully active for the wave-level shadow queries
+        const bool hit = scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
+        if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+        const V3 E = shade<EAGER, DEEP, DL>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, hit);
+        return hit ? E : v3(S.bg[0], S.bg[1], S.bg[2]);
     }
     Frame stk[kMaxDepth];
     int sp = 0;

@@ -144,8 +144,8 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         P.mat[idx] = hits ? h.mat : -3;
         if (P.ext_shade[ei]) {
             // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
-            V3 base = v3(RV(1.0), RV(1.0), RV(1.0));
-            if (hits) base = shade<E, D, DL>(S, ht, h, normalized(vneg(r.d)), no, cnt);
+            V3 base = shade<E, D, DL>(S, ht, h, normalized(vneg(r.d)), no, cnt, hits);
+            if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             P.lum[idx] = RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z;
         }
     }
@@ -251,6 +251,7 @@ DevScene make_scene(const SceneView& V) {
     S.gb = V.gb;
     S.n_lights = V.n_lights;
     S.n_dlights = V.n_dlights;
+    S.n_bounded = V.n_bounded;
     S.n_objs = V.n_objs;
     S.cam_nx = V.cam_nx;
     S.cam_ny = V.cam_ny;

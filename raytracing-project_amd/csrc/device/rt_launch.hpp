@@ -62,6 +62,7 @@ struct SceneView {
     const DevOp* ops;
     const float* gb;
     int n_lights, n_dlights, n_objs;
+    int n_bounded;
     int cam_nx, cam_ny;
     int rec_limit, cull;
     double eye[3], P[3], Lx, Ly;

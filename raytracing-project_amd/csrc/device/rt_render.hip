@@ -325,6 +325,9 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.gb = ws.gb.as<float>();
     S.n_lights = d.n_lights;
     S.n_objs = (int)f->cs.objs.size();
+    S.n_bounded = 0;
+    for (const auto& o : f->cs.objs)
+        if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++S.n_bounded;
     S.cam_nx = rt_camera_width(&d.camera);
     S.cam_ny = rt_camera_height(&d.camera);
     S.rec_limit = d.recursion_limit;
