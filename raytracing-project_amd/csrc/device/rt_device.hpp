@@ -1215,7 +1215,8 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
 // Scene::occluded for the querying lanes of a fully active wave.  Returns
 // false for lanes with need = false.
 template <bool EAGER, bool DEEP, class CT>
-__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, CT& cnt) {
+__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, bool wave_ok,
+                                    CT& cnt) {
     const FRay fr = to_fray(r);
     const float ftmin = (float)tmin, ftmax = (float)tmax;
     const float Ax = __builtin_fmaf(ftmin, fr.dx, fr.ox), Ay = __builtin_fmaf(ftmin, fr.dy, fr.oy),
@@ -1225,18 +1226,17 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
     const bool fin = __builtin_isfinite(Ax + Ay + Az + Bx + By + Bz);
     const uint64_t nm = __ballot(need);
     if (!nm) return false;
-    if (__any(need && !fin)) {   // unbounded or non-finite segments: the per-object loop
-        bool hit = false;
-        if (need) hit = scene_occluded<EAGER, DEEP>(S, r, tmin, tmax, cnt);
-        return hit;
-    }
+    // without the capsule (a partially active wave, or unbounded / non-finite
+    // segments) every object is a candidate and each bounded one gets the
+    // per-lane segment test
+    const bool cap = wave_ok && !__any(need && !fin);
     const int f = __builtin_ctzll(nm);
     const float ax = rdlane_f(Ax, f), ay = rdlane_f(Ay, f), az = rdlane_f(Az, f);
     const float bx = rdlane_f(Bx, f), by = rdlane_f(By, f), bz = rdlane_f(Bz, f);
     float da = (Ax - ax) * (Ax - ax) + (Ay - ay) * (Ay - ay) + (Az - az) * (Az - az);
     float db = (Bx - bx) * (Bx - bx) + (By - by) * (By - by) + (Bz - bz) * (Bz - bz);
     const float d = need ? __builtin_fmaxf(da, db) : 0.0f;
-    const float rho = __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(d))));
+    const float rho = cap ? __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(d)))) : 0.0f;
     const float ux = bx - ax, uy = by - ay, uz = bz - az;
     const float uu = __builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz));
     const float mag = __builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
@@ -1249,9 +1249,12 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         if (j < S.n_objs) {
             const DevObj& ob = S.objs[j];
             pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
-                   (!ob.has_bound || capsule_touch(ob.fb, ax, ay, az, ux, uy, uz, uu, rho, mag));
+                   (!ob.has_bound || !cap || capsule_touch(ob.fb, ax, ay, az, ux, uy, uz, uu, rho, mag));
         }
-        uint64_t m = __ballot(pass);
+        // (lane j tests object j only with the whole wave active; otherwise
+        // every object of the chunk is a candidate)
+        const int nc = S.n_objs - base;
+        uint64_t m = cap ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             if (need) {
                 int skipped = 0;
@@ -1266,7 +1269,8 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             const int o = base + __builtin_ctzll(m);
             m &= m - 1;
             const DevObj ob = S.objs[o];
-            if (ob.kind >= rtamd::OBJ_CHAIN && ob.has_bound) {   // expensive objects: per-lane segment test
+            if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            if (S.cull && ob.has_bound && (!cap || ob.kind >= rtamd::OBJ_CHAIN)) {   // per-lane segment test
                 if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
                     if (need) cnt.inc(RT_OPC_CULLED);
                     continue;
@@ -1282,6 +1286,100 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         }
     }
     return hit;
+}
+
+
+// Scene::intersect for a fully active wave: the closest hit of every lane.
+// The lanes' rays form a bundle - origins within rho of lane 0's, directions
+// within the cone of half-angle theta around lane 0's - and every ray point
+// o_i + t d_i (t >= 0) lies within rho of the cone from lane 0's origin.  One
+// transposed test of object j's ball (grown by rho) against that cone, on
+// lane j, picks the objects any lane can reach; the per-object loop then runs
+// over those, in scene order, exactly as scene_intersect (ties and the
+// shrinking closest-so-far included).  Conservative in f32 like
+// capsule_touch: results are unchanged.
+__device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
+                                          float az, float cth, float sth, float rho, float mag) {
+    const float wx = g[0] - ox, wy = g[1] - oy, wz = g[2] - oz;
+    const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
+    const float R = g[3] + rho + m;
+    const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
+    if (!(L2 > R * R)) return true;   // the bundle's origin region touches the ball (or NaN)
+    const float wa = __builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az));
+    // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R
+    const float rhs = cth * __builtin_sqrtf(L2 - R * R) - sth * R;
+    return !(wa + m < rhs);
+}
+
+template <bool EAGER, bool DEEP, class CT>
+__device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin, real tmax, real& t_best,
+                                     DHit& best, bool wave_ok, CT& cnt) {
+    const FRay fr = to_fray(r);
+    const bool fin = __builtin_isfinite(fr.ox + fr.oy + fr.oz + fr.dx + fr.dy + fr.dz);
+    // no cone for a partially active wave or non-finite rays: every object is
+    // a candidate (the per-lane ball test still runs)
+    const bool cone = wave_ok && !__any(!fin) && tmin >= RV(0.0);
+    const float ox = rdlane_f(fr.ox, 0), oy = rdlane_f(fr.oy, 0), oz = rdlane_f(fr.oz, 0);
+    const float ax = rdlane_f(fr.dx, 0), ay = rdlane_f(fr.dy, 0), az = rdlane_f(fr.dz, 0);
+    const float do2 = (fr.ox - ox) * (fr.ox - ox) + (fr.oy - oy) * (fr.oy - oy) + (fr.oz - oz) * (fr.oz - oz);
+    // 1 - cos(angle to the axis), >= 0 up to rounding
+    const float dc = __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, ax, __builtin_fmaf(fr.dy, ay, fr.dz * az)));
+    const float rho = cone ? __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(do2)))) : 0.0f;
+    const float dcm = cone ? __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f : 2.0f;   // rounding of unit dots
+    const float cth = 1.0f - dcm;
+    const bool wide = !(cth > 0.0f);   // a bundle wider than 90 degrees (or no cone): no culling
+    const float sth = __builtin_sqrtf(__builtin_fmaxf(0.0f, 1.0f - cth * cth)) + 1e-6f;
+    const float mag = __builtin_fabsf(ox) + __builtin_fabsf(oy) + __builtin_fabsf(oz) + rho + 1.0f;
+    const int lane = __lane_id();
+    real closest = tmax;
+    int win = -1;
+    V3 wp = v3(RV(0.0), RV(0.0), RV(0.0));
+    real wts = RV(0.0);
+    int wcode = 0;
+    const float ftmin = (float)tmin;
+    for (int base = 0; base < S.n_objs; base += 64) {
+        const int j = base + lane;
+        bool pass = false;
+        if (j < S.n_objs) {
+            const DevObj& ob = S.objs[j];
+            pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
+                   (!ob.has_bound || wide || cone_touch(ob.fb, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+        }
+        const int nc = S.n_objs - base;
+        uint64_t m = cone ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        if constexpr (!std::is_same<CT, Cnt<false>>::value) {
+            int skipped = 0;
+            for (int o = base; o < S.n_objs && o < base + 64; ++o) {
+                const int k = S.objs[o].kind;
+                if (k != rtamd::OBJ_GROUP && k != rtamd::OBJ_NEVER && !((m >> (o - base)) & 1)) ++skipped;
+            }
+            cnt_add(cnt, RT_OPC_CULLED, skipped);
+        }
+        while (m) {
+            const int o = base + __builtin_ctzll(m);
+            m &= m - 1;
+            const DevObj ob = S.objs[o];
+            if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            if (S.cull && ob.has_bound && !__any(ball_touch(ob.fb, fr, ftmin, (float)closest))) {
+                cnt.inc(RT_OPC_CULLED);
+                continue;
+            }
+            real t = RV(0.0), ts = RV(0.0);
+            V3 p;
+            int code = 0;
+            if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt)) {
+                closest = t;
+                win = o;
+                wp = p;
+                wts = ts;
+                wcode = code;
+            }
+        }
+    }
+    if (win < 0) return false;
+    resolve_hit<EAGER>(S, win, r, tmin, wp, wts, wcode, best, cnt);
+    t_best = closest;
+    return true;
 }
 
 // ----------------------------------------------------------------- shading
@@ -1325,7 +1423,7 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 // never populates directional lights).
 // DL: the scene may have directional lights (the lean kernels, chosen only
 // for scenes without, do not carry their code or registers).
-template <bool EAGER, bool DEEP, bool DL, class CT>
+template <bool EAGER, bool DEEP, bool DL, bool WV, class CT>
 __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt,
                     bool valid = true) {
     // valid = false: a lane of the wave that has nothing to shade (a primary
@@ -1334,9 +1432,9 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
     const bool has_mat = hit.mat >= 0;
     valid = valid && has_mat;
     if (valid) cnt.inc(RT_OPC_SHADE_CALL);
-    // full-wave shadow queries (scene_occluded_wave) need every lane active
-    // (with fewer than 4 bounded objects the per-object wave tests are cheaper)
-    const bool wave_full = S.cull && S.n_bounded >= 4 && __builtin_amdgcn_read_exec() == ~0ull;
+    // WV (wave-level culling; the host picks it for scenes with >= 4 bounded
+    // objects, culling on): the capsule test needs every lane active
+    const bool wave_full = WV && __builtin_amdgcn_read_exec() == ~0ull;
     const V3 n = hit.n;
     const real eps = dmax(RV(1e-3), RV(1e-4) * ht);
     // Two passes over the lights so that only (p, n, eps) stay live across
@@ -1397,10 +1495,10 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
             const DRay sr = make_ray(so, wi);
             bool occ = false;
-            if (wave_full) {
-                occ = scene_occluded_wave<EAGER, DEEP>(S, sr, eps, max_t, need, cnt);
-            } else if (need) {
-                occ = scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt);
+            if constexpr (WV) {
+                occ = scene_occluded_wave<EAGER, DEEP>(S, sr, eps, max_t, need, wave_full, cnt);
+            } else {
+                if (need) occ = scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt);
             }
             if (need) {
                 ++n_occl;
@@ -1455,7 +1553,7 @@ struct Frame {
 };
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
-template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, class CT>
+template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, bool WV, class CT>
 __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     if constexpr (!SECONDARY) {
         // No material reflects or refracts (or recursion <= 1): trace_recursive
@@ -1465,12 +1563,18 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         DHit h;
         h.mat = -1;
         ++n_isect;
-        // miss lanes stay in shade() (valid = false) so that the wave stays
-        // fully active for the wave-level shadow queries
-        const bool hit = scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
-        if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);
-        const V3 E = shade<EAGER, DEEP, DL>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, hit);
-        return hit ? E : v3(S.bg[0], S.bg[1], S.bg[2]);
+        if constexpr (WV) {
+            // miss lanes stay in shade() (valid = false) so that the wave
+            // stays fully active for the wave-level shadow queries
+            const bool hit = scene_intersect_wave<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h,
+                                                               __builtin_amdgcn_read_exec() == ~0ull, cnt);
+            if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+            const V3 E = shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, hit);
+            return hit ? E : v3(S.bg[0], S.bg[1], S.bg[2]);
+        } else {
+            if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+            return shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
+        }
     }
     Frame stk[kMaxDepth];
     int sp = 0;
@@ -1490,7 +1594,7 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
                 ret = v3(S.bg[0], S.bg[1], S.bg[2]);
             } else {
                 const V3 wo = normalized(vneg(r.d));
-                const V3 direct = shade<EAGER, DEEP, DL>(S, ht, h, wo, n_occl, cnt);
+                const V3 direct = shade<EAGER, DEEP, DL, WV>(S, ht, h, wo, n_occl, cnt);
                 if (h.mat < 0) {
                     ret = direct;
                 } else {

@@ -64,7 +64,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #define RT_LEAN_WAVES 4
 #endif
 
-template <bool E, bool D, bool SEC, bool C, bool DL = true>
+template <bool E, bool D, bool SEC, bool C, bool DL = true, bool WV = false>
 __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -82,7 +82,7 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
         // draws 16p+2s, 16p+2s+1 of the stream: dx, dy (tracer.cpp:293)
         const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)P.jrow[ri] * P.W + x) * 16 + 2 * s);
         const DRay ray = gen_ray_subpixel(S, x, y, RV(j.x), RV(j.y));
-        c = trace<E, D, SEC, DL>(S, ray, ni, no, cnt);
+        c = trace<E, D, SEC, DL, WV>(S, ray, ni, no, cnt);
     }
     // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
     const int base = lane & ~7;
@@ -106,18 +106,20 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     flush_counters(P.counters, ni, no, cnt);
 }
 
-template <bool E, bool D, bool SEC, bool C>
+// WV: wave-level culling (scene_occluded_wave / scene_intersect_wave), picked
+// by the host for scenes with >= 4 bounded objects and culling on.
+template <bool E, bool D, bool SEC, bool C, bool WV = false>
 __global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
-    std_body<E, D, SEC, C>(S, P);
+    std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
-template <bool C>
+template <bool C, bool WV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
                                                                                                        StdParams P) {
-    std_body<false, false, false, C, false>(S, P);
+    std_body<false, false, false, C, false, WV>(S, P);
 }
 
-template <bool E, bool D, bool C, bool DL = true>
+template <bool E, bool D, bool C, bool DL = true, bool WV = false>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
@@ -134,7 +136,13 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         real ht = RV(0.0);
         DHit h;
         ++ni;
-        const bool hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
+        h.mat = -1;
+        bool hits;
+        if constexpr (WV)
+            hits = scene_intersect_wave<E, D>(S, r, RV(1e-4), RT_INF, ht, h, __builtin_amdgcn_read_exec() == ~0ull,
+                                              cnt);
+        else
+            hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
         const size_t idx = (size_t)ei * P.W + x;
         P.hit[idx] = hits ? 1 : 0;
         P.t[idx] = ht;
@@ -144,7 +152,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         P.mat[idx] = hits ? h.mat : -3;
         if (P.ext_shade[ei]) {
             // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
-            V3 base = shade<E, D, DL>(S, ht, h, normalized(vneg(r.d)), no, cnt, hits);
+            V3 base = shade<E, D, DL, WV>(S, ht, h, normalized(vneg(r.d)), no, cnt, hits);
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             P.lum[idx] = RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z;
         }
@@ -157,10 +165,10 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
     paper_primary_body<E, D, C>(S, P);
 }
 
-template <bool C>
+template <bool C, bool WV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
-    paper_primary_body<false, false, C, false>(S, P);
+    paper_primary_body<false, false, C, false, WV>(S, P);
 }
 
 // apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
@@ -269,10 +277,10 @@ DevScene make_scene(const SceneView& V) {
     return S;
 }
 
-template <bool E, bool D, bool SEC>
+template <bool E, bool D, bool SEC, bool WV = false>
 void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std<E, D, SEC, false>), grid, dim3(256), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true, WV>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_std<E, D, SEC, false, WV>), grid, dim3(256), 0, st, S, P);
 }
 
 template <bool E, bool D>
@@ -287,6 +295,7 @@ void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const 
 void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const SceneView& V,
                 const StdParams& P) {
     const DevScene S = make_scene(V);
+    const bool wv = V.cull && V.n_bounded >= 4;
     if (e) {
         if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
         else launch_std_c<true, true, false>(c, grid, st, S, P);
@@ -294,18 +303,31 @@ void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, con
         if (sec) launch_std_c<false, true, true>(c, grid, st, S, P);
         else launch_std_c<false, true, false>(c, grid, st, S, P);
     } else {
-        if (sec) launch_std_c<false, false, true>(c, grid, st, S, P);
-        else if (c) hipLaunchKernelGGL((k_std_lean<true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_std_lean<false>), grid, dim3(256), 0, st, S, P);
+        if (sec) {
+            if (wv) launch_std_c<false, false, true, true>(c, grid, st, S, P);
+            else launch_std_c<false, false, true>(c, grid, st, S, P);
+        } else if (wv) {
+            if (c) hipLaunchKernelGGL((k_std_lean<true, true>), grid, dim3(256), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, true>), grid, dim3(256), 0, st, S, P);
+        } else {
+            if (c) hipLaunchKernelGGL((k_std_lean<true, false>), grid, dim3(256), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, false>), grid, dim3(256), 0, st, S, P);
+        }
     }
 }
 
 void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const SceneView& V, const PaperParams& P) {
     const DevScene S = make_scene(V);
+    const bool wv = V.cull && V.n_bounded >= 4;
     if (e) launch_paper_c<true, true>(c, grid, st, S, P);
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
-    else if (c) hipLaunchKernelGGL((k_paper_primary_lean<true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_paper_primary_lean<false>), grid, dim3(256), 0, st, S, P);
+    else if (wv) {
+        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, true>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, true>), grid, dim3(256), 0, st, S, P);
+    } else {
+        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, false>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, false>), grid, dim3(256), 0, st, S, P);
+    }
 }
 
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {

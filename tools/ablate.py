@@ -38,7 +38,8 @@ def run(name, scene, mode=0, flags=0, reps=2):
 def main():
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     base = json.loads(scenes.config_json(cfg)[0])
-    run("full", base, reps=3)
+    mode = scenes.config_json(cfg)[1]
+    run("full" + (" (paper)" if mode else ""), base, mode=mode, reps=3)
     if os.environ.get("ABLATE_QUICK"):
         return
     run("full no-cull", base, flags=rtamd.RT_FLAG_NO_CULL)
