@@ -1270,7 +1270,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
-            if (S.cull && ob.has_bound && (!cap || ob.kind >= rtamd::OBJ_CHAIN)) {   // per-lane segment test
+            if (S.cull && ob.has_bound) {   // per-lane segment test (f32, cheaper than an FP64 miss)
                 if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
                     if (need) cnt.inc(RT_OPC_CULLED);
                     continue;
