@@ -6,4 +6,4 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; tail gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-TAG=r01b bash tools/profile_bench.sh && echo profiled
+TAG=${TAG:-r01c} bash tools/profile_bench.sh && echo profiled

@@ -31,13 +31,16 @@ def main(src, dst, tag):
             continue
         pmc[name] = {c: sum(v) / len(v) for c, v in cs.items()}   # mean per dispatch
     json.dump(pmc, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    trace = [n for n in pmc if "k_std" in n and "true>" not in n.split("k_std")[1].split(")")[0][-6:]]
-    main_k = None
-    for n in pmc:
-        if "k_std<false, false, false, false>" in n:
-            main_k = n
-    if main_k is None and trace:
-        main_k = trace[0]
+    def uncounted_trace(n):
+        # the timed trace kernel: k_std_lean<C, WV> / k_std<E, D, SEC, C, WV> with C = false
+        for key, pos in (("k_std_lean<", 0), ("k_std<", 3)):
+            if key in n:
+                args = [a.strip() for a in n.split(key, 1)[1].split(">", 1)[0].split(",")]
+                return len(args) > pos and args[pos] == "false"
+        return False
+
+    cands = [n for n in pmc if uncounted_trace(n)]
+    main_k = max(cands, key=lambda n: pmc[n].get("SQ_WAVES", 0.0)) if cands else None
     if main_k and "FETCH_SIZE" in pmc[main_k] and "WRITE_SIZE" in pmc[main_k]:
         f, w = pmc[main_k]["FETCH_SIZE"], pmc[main_k]["WRITE_SIZE"]
         out = {"config": 4, "kernel": main_k, "fetch_kib_raw": f, "write_kib": w,
