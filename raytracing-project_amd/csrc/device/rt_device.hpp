@@ -1270,6 +1270,12 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            // CSG objects: no lane's segment reaches a leaf ball (DevObj::pb0)
+            if (cap && ob.npb > 0 &&
+                !__any(lane < ob.npb && capsule_touch(S.gb + 4 * (ob.pb0 + lane), ax, ay, az, ux, uy, uz, uu, rho, mag))) {
+                if (need) cnt.inc(RT_OPC_CULLED);
+                continue;
+            }
             if (S.cull && ob.has_bound) {   // per-lane segment test (f32, cheaper than an FP64 miss)
                 if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
                     if (need) cnt.inc(RT_OPC_CULLED);
@@ -1318,7 +1324,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     const bool fin = __builtin_isfinite(fr.ox + fr.oy + fr.oz + fr.dx + fr.dy + fr.dz);
     // no cone for a partially active wave or non-finite rays: every object is
     // a candidate (the per-lane ball test still runs)
-    const bool cone = wave_ok && !__any(!fin) && tmin >= RV(0.0);
+    const bool cone = S.cull && wave_ok && !__any(!fin) && tmin >= RV(0.0);
     const float ox = rdlane_f(fr.ox, 0), oy = rdlane_f(fr.oy, 0), oz = rdlane_f(fr.oz, 0);
     const float ax = rdlane_f(fr.dx, 0), ay = rdlane_f(fr.dy, 0), az = rdlane_f(fr.dz, 0);
     const float do2 = (fr.ox - ox) * (fr.ox - ox) + (fr.oy - oy) * (fr.oy - oy) + (fr.oz - oz) * (fr.oz - oz);
@@ -1360,6 +1366,12 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            // CSG objects: the bundle reaches no leaf ball (DevObj::pb0)
+            if (!wide && ob.npb > 0 &&
+                !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + lane), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
+                cnt.inc(RT_OPC_CULLED);
+                continue;
+            }
             if (S.cull && ob.has_bound && !__any(ball_touch(ob.fb, fr, ftmin, (float)closest))) {
                 cnt.inc(RT_OPC_CULLED);
                 continue;

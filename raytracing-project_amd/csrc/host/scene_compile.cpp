@@ -65,9 +65,60 @@ bool is_degenerate_scaling(const rt_node& n) {
            (std::fabs(n.v[0]) < kEPS || std::fabs(n.v[5]) < kEPS || std::fabs(n.v[10]) < kEPS);
 }
 
+// The ball b of a transform node's child, in the node's parent frame.
+Bound xform_ball(const rt_node& n, const Bound& b) {
+    if (b.kind != Bound::Ball) return b;
+    if (n.kind == RT_NODE_TRANSLATION) return ball(b.c[0] + n.v[3], b.c[1] + n.v[7], b.c[2] + n.v[11], b.r);
+    if (n.kind == RT_NODE_SCALING) {
+        double s = std::max(std::fabs(n.v[0]), std::max(std::fabs(n.v[5]), std::fabs(n.v[10])));
+        return ball(b.c[0] * n.v[0], b.c[1] * n.v[5], b.c[2] * n.v[10], b.r * s);
+    }
+    const double* M = n.v;   // rotation
+    return ball(M[0] * b.c[0] + M[1] * b.c[1] + M[2] * b.c[2] + M[3],
+                M[4] * b.c[0] + M[5] * b.c[1] + M[6] * b.c[2] + M[7],
+                M[8] * b.c[0] + M[9] * b.c[1] + M[10] * b.c[2] + M[11], b.r);
+}
+
 class Compiler {
 public:
     explicit Compiler(const rt_scene_desc& d) : d_(d) {}
+
+    // Height of the CSG tree rooted at idx (0 for a leaf).
+    int csg_height(int idx, int level = 0) {
+        if (level > 4096) throw std::runtime_error("scene graph too deep");
+        const rt_node& n = d_.nodes[idx];
+        if (n.kind != RT_NODE_CSG) return 0;
+        return 1 + std::max(csg_height(n.a, level + 1), csg_height(n.b, level + 1));
+    }
+
+    // Leaf prefilter of a CHAIN object with a compact CSG core (ops
+    // [cpc0, cpc1)): a hit of the object lies at a point of the CSG's first
+    // interval, and every point of a CSG interval is within height x 1e-6 (the
+    // event comparator's tie width, once per level) of some leaf interval,
+    // i.e. of a leaf's ball - the result's events are leaf events or the
+    // origin, which then lies inside a leaf (csg.cpp:61-163).  So a segment
+    // that passes no leaf ball grown by that slop cannot hit the object.  The
+    // balls are mapped through the transform chain to the world frame.
+    void leaf_prefilter(DevObj& o, const std::vector<int>& chain, int core, CompiledScene& cs) {
+        std::vector<int> leaves;
+        for (int pc = o.cpc0; pc < o.cpc1; ++pc)
+            if (cs.ops[pc].op == OP_LEAF_IVL) leaves.push_back(cs.ops[pc].node);
+        if (leaves.empty() || leaves.size() > 64) return;
+        const double slop = (csg_height(core) + 2) * 1e-6;
+        std::vector<float> balls;
+        for (int lf : leaves) {
+            Bound b = bound(lf);
+            if (b.kind != Bound::Ball) return;   // a half-space leaf: no prefilter
+            b.r += slop;
+            for (size_t k = chain.size(); k-- > 0;) b = xform_ball(d_.nodes[chain[k]], b);
+            float fb[4];
+            float_ball(b.c, b.r, fb);
+            balls.insert(balls.end(), fb, fb + 4);
+        }
+        o.pb0 = (int)(cs.gbounds.size() / 4);
+        o.npb = (int)leaves.size();
+        cs.gbounds.insert(cs.gbounds.end(), balls.begin(), balls.end());
+    }
 
     Bound bound(int idx, int level = 0) {
         if (level > 4096) throw std::runtime_error("scene graph too deep");
@@ -78,26 +129,11 @@ public:
                 return ball(n.v[0], n.v[1], n.v[2], n.v[3]);
             case RT_NODE_HALFSPACE:
                 return Bound{};
-            case RT_NODE_TRANSLATION: {
-                Bound b = bound(n.a, level + 1);
-                if (b.kind != Bound::Ball) return b;
-                return ball(b.c[0] + n.v[3], b.c[1] + n.v[7], b.c[2] + n.v[11], b.r);
-            }
-            case RT_NODE_SCALING: {
+            case RT_NODE_TRANSLATION:
+            case RT_NODE_SCALING:
+            case RT_NODE_ROTATION:
                 if (is_degenerate_scaling(n)) { Bound e; e.kind = Bound::Empty; return e; }
-                Bound b = bound(n.a, level + 1);
-                if (b.kind != Bound::Ball) return b;
-                double s = std::max(std::fabs(n.v[0]), std::max(std::fabs(n.v[5]), std::fabs(n.v[10])));
-                return ball(b.c[0] * n.v[0], b.c[1] * n.v[5], b.c[2] * n.v[10], b.r * s);
-            }
-            case RT_NODE_ROTATION: {
-                Bound b = bound(n.a, level + 1);
-                if (b.kind != Bound::Ball) return b;
-                const double* M = n.v;
-                return ball(M[0] * b.c[0] + M[1] * b.c[1] + M[2] * b.c[2] + M[3],
-                            M[4] * b.c[0] + M[5] * b.c[1] + M[6] * b.c[2] + M[7],
-                            M[8] * b.c[0] + M[9] * b.c[1] + M[10] * b.c[2] + M[11], b.r);
-            }
+                return xform_ball(n, bound(n.a, level + 1));
             case RT_NODE_CSG: {
                 Bound a = bound(n.a, level + 1), b = bound(n.b, level + 1);
                 if (n.op == RT_CSG_UNION) return merge_union(a, b);
@@ -338,6 +374,7 @@ public:
                 }
                 o.cpc1 = (int)cs.ops.size();
                 o.pc1 = o.cpc1;
+                if (!leaf_core) leaf_prefilter(o, chain, core, cs);
             } else {
                 o.kind = OBJ_EAGER;
                 cs.has_eager = true;

@@ -55,6 +55,8 @@ struct DevObj {
     int32_t cpc0, cpc1; // CHAIN: leaf core -> cpc0 = its LEAF_ISECT op; CSG core -> [cpc0,cpc1) compact program
     int32_t pc1;        // EAGER: program end
     int32_t has_bound;  // conservative world-space bounding sphere present
+    int32_t pb0;        // CHAIN with a compact CSG core: first leaf prefilter ball in gbounds (units of 4 floats)
+    int32_t npb;        //   and their count (0 = none): world balls of every leaf, grown by the CSG epsilon slop
     int32_t pad;
     double bc[3];       // bound centre
     double br;          // bound radius (already inflated)
@@ -71,7 +73,8 @@ struct DevOp {
 struct CompiledScene {
     std::vector<DevObj> objs;
     std::vector<DevOp> ops;
-    std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated
+    std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated;
+                                   // then the leaf prefilter balls of CHAIN objects (world frame, see DevObj::pb0)
     int max_ray_depth = 0;   // transform nesting on any path
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter
