@@ -4,7 +4,7 @@
 // uniform_real_distribution<double>(-0.5,0.5) (raytracer/src/tracer.cpp:
 // 284-293; libstdc++ generate_canonical, random.tcc:3348-3378).  Here the
 // stream is cut into segments of K twist blocks.  k_mt_jump computes the
-// window at every segment start with a radix-8 tree of GF(2) jumps
+// window at every segment start with a radix-64 tree of GF(2) jumps
 // (csrc/host/mt_poly.cpp: window' = XOR_i p_i * window shifted by i), each
 // jump split over S workgroups by tap ranges; k_mt_fill regenerates every
 // segment inside one workgroup and writes the jitter doubles.  Output:
@@ -71,15 +71,15 @@ __device__ __forceinline__ void lds_barrier() {
 
 __device__ __forceinline__ int ckpt_parts(int64_t c, const int8_t* parts) {
     if (c == 0) return 1;
-    const int j = (63 - __builtin_clzll((unsigned long long)c)) / 3;   // c in [8^j, 8^(j+1))
+    const int j = (63 - __builtin_clzll((unsigned long long)c)) / rtamd::kMTRadixBits;   // c in [R^j, R^(j+1))
     return parts[j];
 }
 
 struct JumpArgs {
-    int64_t lo;                 // 8^j: this level computes checkpoints in [lo, 8*lo)
+    int64_t lo;                 // R^j: this level computes checkpoints in [lo, R*lo)
     const int64_t* list;        // the checkpoints of this level to compute (gridDim.x of them)
     int S;                      // partial jumps per checkpoint (gridDim.y)
-    int32_t off[8], len[8];     // tap slice of x^(624*K*m*8^j), m = c / lo
+    int32_t off[rtamd::kMTRadix], len[rtamd::kMTRadix];   // tap slice of x^(624*K*m*R^j), m = c / lo
     int8_t parts[MAX_LEVELS];   // partial count of the checkpoints of every level
 };
 
@@ -248,10 +248,10 @@ int level_parts(int64_t n_level) {
     return (int)std::min<int64_t>(rtamd::kMTParts, std::max<int64_t>(1, want));
 }
 
-// Level of checkpoint c >= 1 in the radix-8 tree and its parent.
-inline int ckpt_level(int64_t c) { return (63 - __builtin_clzll((unsigned long long)c)) / 3; }
+// Level of checkpoint c >= 1 in the radix-R tree and its parent.
+inline int ckpt_level(int64_t c) { return (63 - __builtin_clzll((unsigned long long)c)) / rtamd::kMTRadixBits; }
 inline int64_t ckpt_parent(int64_t c) {
-    const int64_t lo = (int64_t)1 << (3 * ckpt_level(c));
+    const int64_t lo = (int64_t)1 << (rtamd::kMTRadixBits * ckpt_level(c));
     return c - (c / lo) * lo;
 }
 
@@ -339,8 +339,8 @@ hipError_t mt_launch_jitter(const JitterPlan& plan, const std::vector<JRange>& r
     std::vector<int64_t> lists;
     int64_t lvl_off[MAX_LEVELS + 1] = {0};
     for (int j = 0; j < plan.levels; ++j) {
-        const int64_t lo = (int64_t)1 << (3 * j);
-        for (int64_t c = lo; c <= std::min(c1, lo * 8 - 1); ++c)
+        const int64_t lo = (int64_t)1 << (kMTRadixBits * j);
+        for (int64_t c = lo; c <= std::min(c1, lo * kMTRadix - 1); ++c)
             if (need[c]) lists.push_back(c);
         lvl_off[j + 1] = (int64_t)lists.size();
     }
@@ -370,12 +370,12 @@ hipError_t mt_launch_jitter(const JitterPlan& plan, const std::vector<JRange>& r
         const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
         if (n_j <= 0) continue;
         JumpArgs A;
-        A.lo = (int64_t)1 << (3 * j);
+        A.lo = (int64_t)1 << (kMTRadixBits * j);
         A.list = dL + lvl_off[j];
         A.S = parts[j];
-        for (int m = 0; m < 8; ++m) {
-            A.off[m] = plan.off[(size_t)j * 8 + m];
-            A.len[m] = plan.off[(size_t)j * 8 + m + 1] - A.off[m];
+        for (int m = 0; m < kMTRadix; ++m) {
+            A.off[m] = plan.off[(size_t)j * kMTRadix + m];
+            A.len[m] = plan.off[(size_t)j * kMTRadix + m + 1] - A.off[m];
         }
         for (int k = 0; k < MAX_LEVELS; ++k) A.parts[k] = parts[k];
         hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_j, (unsigned)A.S), dim3(JUMP_THREADS), 0, stream,
@@ -403,7 +403,7 @@ int mt_levels_needed(int K, int64_t q1) {
     const int64_t seg = (int64_t)K * N;
     const int64_t cmax = q1 > 0 ? (q1 - 1) / seg : 0;   // highest checkpoint index
     int L = 1;
-    while (((int64_t)1 << (3 * L)) <= cmax) ++L;
+    while (((int64_t)1 << (kMTRadixBits * L)) <= cmax) ++L;
     return L;
 }
 

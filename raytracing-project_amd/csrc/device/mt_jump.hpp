@@ -14,15 +14,15 @@ namespace rtamd {
 constexpr int kMTParts = 8;
 constexpr int kMTMaxLevels = 8;
 
-// Host-built plan for one segment length K: the radix-8 tree's tap lists
-// (exponents with coefficient 1 in x^(624*K*m*8^j) mod phi, csrc/host/
+// Host-built plan for one segment length K: the radix-64 tree's tap lists
+// (exponents with coefficient 1 in x^(624*K*m*64^j) mod phi, csrc/host/
 // mt_poly.cpp) and the seed window, resident on the device.
 struct JitterPlan {
     int K = 0;
     int levels = 0;
     uint16_t* d_taps = nullptr;
     uint32_t* d_base = nullptr;        // window at n = 624 for seed 12345
-    std::vector<int32_t> off;          // taps of (j, m) at [off[j*8+m], off[j*8+m+1]), m in 1..7
+    std::vector<int32_t> off;          // taps of (j, m) at [off[j*R+m], off[j*R+m+1]), m in 1..R-1
     hipError_t build(int K_blocks, int levels_needed);   // synchronous upload
     void release();
 };

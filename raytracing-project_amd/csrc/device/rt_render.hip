@@ -643,8 +643,8 @@ extern "C" int rt_framebuffer_to_rgb8_device(const double* fb_dev, size_t n_pixe
 #include "rt_test.h"
 
 extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
-    // Every radix-8 tree polynomial x^(624*K*m*8^j) applied to the seed
-    // window must equal advancing it m*8^j*K twist blocks sequentially.
+    // Every radix-R tree polynomial x^(624*K*m*R^j) applied to the seed
+    // window must equal advancing it m*R^j*K twist blocks sequentially.
     try {
         std::vector<uint32_t> polys = rtamd::mt_tree_polys(K_blocks, levels);
         uint32_t base[624];
@@ -653,11 +653,12 @@ extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
         for (int j = 0; j < levels; ++j) {
             uint32_t seq[624];
             std::memcpy(seq, base, sizeof(seq));
-            const uint64_t step = (uint64_t)K_blocks << (3 * j);
+            const uint64_t step = (uint64_t)K_blocks << (rtamd::kMTRadixBits * j);
             for (int m = 1; m < rtamd::kMTRadix; ++m) {
                 rtamd::mt_advance_blocks_cpu(seq, step);
                 uint32_t jumped[624];
-                rtamd::mt_apply_jump_cpu(polys.data() + ((size_t)j * 7 + (m - 1)) * 624, base, jumped);
+                rtamd::mt_apply_jump_cpu(polys.data() + ((size_t)j * (rtamd::kMTRadix - 1) + (m - 1)) * 624, base,
+                                         jumped);
                 // bit 31..0 of words 1..623 and the top bit of word 0 define the state
                 bool ok = (jumped[0] & 0x80000000u) == (seq[0] & 0x80000000u);
                 for (int k = 1; k < 624; ++k) ok = ok && jumped[k] == seq[k];

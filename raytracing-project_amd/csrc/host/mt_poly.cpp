@@ -278,7 +278,7 @@ std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels) {
         std::lock_guard<std::mutex> lk(g_mu);
         if (!R) R = new Reducer(phi);
     }
-    // base = x^(624*K*8^j), level by level (8^j -> 8^(j+1): three squarings)
+    // base = x^(624*K*R^j), level by level (R^j -> R^(j+1): log2(R) squarings)
     std::vector<uint32_t> b0 = mt_jump_table(K_blocks, 1);
     std::vector<uint64_t> base = from_words32(b0.data(), phi.size());
     std::vector<uint32_t> out;

@@ -33,11 +33,14 @@ const std::vector<uint64_t>& mt_charpoly();
 // Cached per (K, levels) in the process.
 std::vector<uint32_t> mt_jump_table(int K_blocks, int levels);
 
-// Radix-8 checkpoint tree (mt_jump.hip): level j computes checkpoints
-// c in [8^j, 8^(j+1)) as ONE jump from c - m*8^j, m = c / 8^j, by
-// x^(624*K*m*8^j) mod phi.  Returns those polynomials for j < levels and
-// m = 1..7 at index (j*7 + m-1)*kPolyWords32.  Cached per (K, levels).
-constexpr int kMTRadix = 8;
+// Radix-64 checkpoint tree (mt_jump.hip): level j computes checkpoints
+// c in [64^j, 64^(j+1)) as ONE jump from c - m*64^j, m = c / 64^j, by
+// x^(624*K*m*64^j) mod phi.  Returns those polynomials for j < levels and
+// m = 1..63 at index (j*63 + m-1)*kPolyWords32.  Cached per (K, levels).
+// (Radix 64: two levels reach 4096 segments - every frame up to 8K - so a
+// frame's checkpoints take two dependent jump launches.)
+constexpr int kMTRadixBits = 6;
+constexpr int kMTRadix = 1 << kMTRadixBits;
 std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels);
 
 // x^J mod phi for an arbitrary J (kPolyWords32 words).

@@ -79,7 +79,7 @@ def test_to_rgb8_matches_toByte(rt):
 
 def test_mt19937_jump_polynomials_cpu():
     amd = C.CDLL(os.path.join(LIB, "librtamd.so"), mode=C.RTLD_GLOBAL)
-    assert amd.rt_test_mt_jump_cpu(1024, 2) == 0   # radix-8 tree: m*8^j*K blocks, j < 2
+    assert amd.rt_test_mt_jump_cpu(64, 2) == 0   # radix-64 tree: m*64^j*K blocks, j < 2
     assert amd.rt_test_mt_jump_cpu(3, 3) == 0   # non power-of-two segment length
 
 
