@@ -1248,8 +1248,20 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         bool pass = false;
         if (j < S.n_objs) {
             const DevObj& ob = S.objs[j];
-            pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
-                   (!ob.has_bound || !cap || capsule_touch(ob.fb, ax, ay, az, ux, uy, uz, uu, rho, mag));
+            if (ob.kind == rtamd::OBJ_HALF && cap) {
+                // a bare half-space: the segments cross its plane only if the
+                // capsule does (both axis ends farther than rho on one side: no lane)
+                const NodeT* nd = &S.nodes[ob.node];
+                const float nx = (float)nd->v[3], ny = (float)nd->v[4], nz = (float)nd->v[5];
+                const float px = (float)nd->v[0], py = (float)nd->v[1], pz = (float)nd->v[2];
+                const float sa = nx * (ax - px) + ny * (ay - py) + nz * (az - pz);
+                const float sb = nx * (bx - px) + ny * (by - py) + nz * (bz - pz);
+                const float m = rho + 1e-5f * (mag + __builtin_fabsf(px) + __builtin_fabsf(py) + __builtin_fabsf(pz));
+                pass = !((sa > m && sb > m) || (sa < -m && sb < -m));   // NaN passes
+            } else {
+                pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
+                       (!ob.has_bound || !cap || capsule_touch(ob.fb, ax, ay, az, ux, uy, uz, uu, rho, mag));
+            }
         }
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
