@@ -68,6 +68,35 @@ def test_midres_matches_oracle(gpu, name):
     assert st.rays_occluded == ost.rays_occluded
 
 
+def _odd_size(text, w, h, dpi=16):
+    """Same scene and screen centre, a W x H frame that leaves partial waves
+    and blocks at the right and bottom edges (W, H exact multiples of 1/dpi)."""
+    d = json.loads(text)
+    scr = d["screen"]
+    dims = scr.get("dimensions", [1, 1])
+    cx, cy = scr["position"][0] + dims[0] / 2, scr["position"][1] + dims[1] / 2
+    scr["dpi"] = dpi
+    scr["dimensions"] = [w / dpi, h / dpi]
+    scr["position"] = [cx - w / dpi / 2, cy - h / dpi / 2, scr["position"][2]]
+    return json.dumps(d)
+
+
+# Partial waves (frame edges) take the per-object fallback of the wave-culled
+# kernels (WV): scenes with >= 4 bounded objects at sizes that are not
+# multiples of the 8x4 / 16x16 pixel blocks.
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg4", "cfg5", "snorlax", "csg_groups"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_partial_waves_match_oracle(gpu, name, mode):
+    fb, ref, st, ost = _compare(gpu, _odd_size(SMALL[name](), 55, 25), mode)
+    assert fb.shape[:2] == (25, 55)
+    assert np.abs(fb - ref).max() <= TOL
+    assert st.rays_intersect == ost.rays_intersect
+    assert st.rays_occluded == ost.rays_occluded
+    if mode == 1:
+        assert np.array_equal(fb, ref)
+
+
 @pytest.mark.gpu
 def test_no_cull_flag_same_image(gpu):
     text = SMALL["snorlax"]()
