@@ -42,6 +42,7 @@ using NodeT = rtamd::NodeR<real>;
 using MatT = rtamd::MatR<real>;
 using LightT = rtamd::LightR<real>;
 using DLightT = rtamd::DLightR<real>;
+using FoldT = rtamd::FoldLeafR<real>;
 #define RV(x) static_cast<real>(x)
 #define RT_INF static_cast<real>(__builtin_inf())
 
@@ -107,11 +108,63 @@ struct THit {   // intersect-mode hit
 };
 
 // Per-lane op counters (RT_FLAG_COUNT_OPS builds only).
+//
+// Diagnostic builds with -DRT_PHASE_PROF (tools/build_exp.sh, never the
+// product library) give the uncounted variant wave-level phase timers:
+// pb(k)/pe(k) bracket a phase at points where the whole wave is converged,
+// and the accumulated shader-clock cycles of lane 0 land in rt_stats.ops[k]
+// (PH_* below).
+enum RtPhase {
+    PH_SETUP = 0,      // jitter load + camera ray
+    PH_PRIMARY,        // scene_intersect(_wave) incl. resolve_hit
+    PH_SHADE1,         // light loop pass 1 without the occlusion queries
+    PH_SHADOW,         // scene_occluded(_wave)
+    PH_SHADOW_CSG,     //   of which compact-CSG object evaluations
+    PH_SHADE2,         // light loop pass 2 (accumulation)
+    PH_PRIMARY_CSG,    // compact-CSG object evaluations of primary rays
+    PH_TAIL,           // sample sum, framebuffer store
+    PH_CSG_LEAF,       // run_compact: leaf intervals
+    PH_CSG_COMB,       // run_compact: CSG combines
+    PH_CHAIN_XF,       // object_hit: transform chain down and back up
+    PH_OBJ_PREF,       // wave queries: per-candidate prefilters (leaf masks, ball tests)
+    PH_OBJ_HIT,        // wave queries: object_hit calls (all kinds)
+    PH_WAVE_SETUP,     // wave queries: bundle setup + transposed object test
+    PH_COUNT
+};
 template <bool C>
 struct Cnt;
 template <>
 struct Cnt<false> {
     __device__ __forceinline__ void inc(int) {}
+#ifdef RT_PHASE_PROF
+    // per-wave accumulators in LDS, updated by the first active lane, so
+    // that phases inside divergent code are timed too (256-thread blocks)
+    // (start stamps live in LDS too: no VGPRs taken from the kernel)
+    __device__ static unsigned long long* acc() {
+        __shared__ unsigned long long a[4][2 * PH_COUNT];
+        return &a[threadIdx.x >> 6][0];
+    }
+    __device__ __forceinline__ void init() {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < PH_COUNT; ++k) acc()[k] = 0;
+    }
+    __device__ __forceinline__ bool first() {
+        return (int)__lane_id() == __builtin_ctzll(__builtin_amdgcn_read_exec());
+    }
+    __device__ __forceinline__ void pb(int k) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (first()) acc()[PH_COUNT + k] = t;
+    }
+    __device__ __forceinline__ void pe(int k) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (first()) acc()[k] += t - acc()[PH_COUNT + k];
+    }
+    __device__ __forceinline__ unsigned long long get(int k) { return acc()[k]; }
+#else
+    __device__ __forceinline__ void init() {}
+    __device__ __forceinline__ void pb(int) {}
+    __device__ __forceinline__ void pe(int) {}
+#endif
 };
 template <>
 struct Cnt<true> {
@@ -121,6 +174,9 @@ struct Cnt<true> {
         for (int i = 0; i < 16; ++i) c[i] = 0;
     }
     __device__ __forceinline__ void inc(int k) { c[k]++; }
+    __device__ __forceinline__ void init() {}
+    __device__ __forceinline__ void pb(int) {}
+    __device__ __forceinline__ void pe(int) {}
 };
 
 struct DevScene {
@@ -131,6 +187,7 @@ struct DevScene {
     const DevObj* objs;
     const DevOp* ops;
     const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
+    const FoldT* fold;  // fold objects' leaf tables (DevObj::fold0)
     int n_lights, n_objs;
     int n_dlights;
     int n_bounded;   // objects with a bounding ball (wave-level culling pays only when > 0)
@@ -886,11 +943,20 @@ __device__ __forceinline__ bool ball_touch(const float* g, const FRay& r, float 
     return !(q2 > R * R);
 }
 
-// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
+// Compact CSG program [pc0, pc1) on the frame ray r: the root interval.
 // The top two stack entries are plain locals (VGPRs); only trees that are
 // not left-deep folds touch the spill array (scratch), at uniform indices.
+//
+// Leaf line mask (lmask, wave-uniform; all ones = none): bit k clear means
+// that no lane's LINE meets the k-th leaf's ball (k = order of the program's
+// OP_LEAF_IVL ops = DevObj::pb0 ball order), so every lane's interval of that
+// leaf is empty (Sphere::interval, geometry.cpp:48-78: disc < 0) and the leaf
+// is pushed as the empty interval without its FP64 evaluation; an operand
+// group whose leaves are all clear is skipped as one empty combine.  Exact by
+// construction: an empty interval is what the skipped evaluation returns.
 template <bool DEEP, class CT>
-__device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1, const DRay& r, CT& cnt) {
+__device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1, const DRay& r, CT& cnt,
+                                            uint64_t lmask = ~0ull, bool use_mask = false) {
     CIvl tos, nos;
     tos.ok = nos.ok = 0;
     tos.t0 = tos.t1 = tos.s0 = tos.s1 = nos.t0 = nos.t1 = nos.s0 = nos.s1 = RV(0.0);
@@ -899,12 +965,23 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
     real sp_t0[NSP], sp_t1[NSP], sp_s0[NSP], sp_s1[NSP];
     int sp_ok[NSP], sp_c0[NSP], sp_c1[NSP];
     int sp = 0;   // stack entries (wave-uniform)
+    int li = 0;   // leaf ordinal (wave-uniform)
     const FRay fr = to_fray(r);
     for (int pc = pc0; pc < pc1; ++pc) {
         const DevOp op = S.ops[pc];
         if (op.op == rtamd::OP_LEAF_IVL) {
             CIvl v;
-            leaf_ivl_c(&S.nodes[op.node], pc, r, v, cnt);
+            if (use_mask && !((lmask >> (li & 63)) & 1ull)) {
+                cnt.inc(RT_OPC_CULLED);
+                v.ok = 0;
+                v.t0 = v.t1 = v.s0 = v.s1 = RV(0.0);
+                v.c0 = v.c1 = 0;
+            } else {
+                cnt.pb(PH_CSG_LEAF);
+                leaf_ivl_c(&S.nodes[op.node], pc, r, v, cnt);
+                cnt.pe(PH_CSG_LEAF);
+            }
+            ++li;
             if (DEEP && sp >= 2) {
                 const int k = sp - 2;
                 sp_ok[k] = nos.ok; sp_t0[k] = nos.t0; sp_t1[k] = nos.t1; sp_s0[k] = nos.s0; sp_s1[k] = nos.s1;
@@ -915,7 +992,11 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
             ++sp;
         } else if (op.op == rtamd::OP_IVL_GROUP) {
             // the full line: Primitive::interval has no range
-            if (S.cull && !__any(ball_touch(S.gb + 4 * op.node, fr, -RT_INF_F, RT_INF_F))) {
+            const int nl = op.top / 2;   // leaves of the group (leaf + CSG op each)
+            const bool skip = use_mask ? ((lmask >> (li & 63)) & ((nl >= 64) ? ~0ull : ((1ull << nl) - 1))) == 0
+                                       : (S.cull && !__any(ball_touch(S.gb + 4 * op.node, fr, -RT_INF_F, RT_INF_F)));
+            if (skip) {
+                li += nl;
                 cnt.inc(RT_OPC_CULLED);
                 CIvl e, v;
                 e.ok = 0;
@@ -927,7 +1008,9 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
             }
         } else {
             CIvl v;
+            cnt.pb(PH_CSG_COMB);
             csg_c(op.csg_op, nos, tos, v, cnt);
+            cnt.pe(PH_CSG_COMB);
             tos = v;
             if (DEEP && sp >= 3) {
                 const int k = sp - 3;
@@ -938,6 +1021,67 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
         }
     }
     return tos;
+}
+
+// Sphere::interval (geometry.cpp:48-78) of a fold leaf, compact form.
+template <class CT>
+__device__ __forceinline__ void fold_leaf_ivl(const FoldT& L, const DRay& r, CIvl& o, CT& cnt) {
+    cnt.inc(RT_OPC_SPHERE_IVL);
+    o.c0 = L.pc;
+    o.c1 = L.pc | REF_ROOT1;
+    const real r0 = L.r;
+    V3 oc = v3(r.o.x - L.c[0], r.o.y - L.c[1], r.o.z - L.c[2]);
+    const real half_b = dot3(oc, r.d);
+    const real cterm = dot3(oc, oc) - r0 * r0;
+    const real disc = half_b * half_b - RV(1.0) * cterm;
+    o.ok = !(disc < RV(0.0));
+    const real sq = sqrt_r(o.ok ? disc : RV(0.0));
+    real t0 = (-half_b - sq) / RV(1.0);
+    real t1 = (-half_b + sq) / RV(1.0);
+    if (t0 > t1) {
+        const real tt = t0;
+        t0 = t1;
+        t1 = tt;
+    }
+    o.t0 = o.s0 = t0;
+    o.t1 = o.s1 = t1;
+    if (o.ok) cnt.inc(RT_OPC_SPHERE_IVL_HIT);
+}
+
+// CSG::interval of a fold object (DevObj::nfold > 0): the left-deep fold
+// acc = leaf_0 op leaf_1 op ... (csg.cpp:61-163, combined by csg_c exactly
+// as run_compact would), with lmask (wave-uniform) naming the leaves some
+// lane's line can meet.  A leaf outside the mask has an empty interval in
+// every lane, so it is not evaluated; combining with an empty interval is
+// idempotent (csg_c: acc op empty = f(acc), f(f(acc)) = f(acc)), so a run of
+// such leaves costs one empty combine.  Exact by construction.
+template <class CT>
+__device__ __forceinline__ CIvl run_fold(const DevScene& S, const DevObj& ob, const DRay& r, uint64_t lmask,
+                                         CT& cnt) {
+    const FoldT* L = S.fold + ob.fold0;
+    CIvl acc, e;
+    e.ok = 0;
+    e.t0 = e.t1 = e.s0 = e.s1 = RV(0.0);
+    e.c0 = e.c1 = 0;
+    if (lmask & 1ull) fold_leaf_ivl(L[0], r, acc, cnt);
+    else acc = e;
+    bool norm = false;   // acc is already a fixed point of the empty combine (wave-uniform)
+    for (int k = 1; k < ob.nfold; ++k) {
+        CIvl v;
+        if (!((lmask >> k) & 1ull)) {
+            cnt.inc(RT_OPC_CULLED);
+            if (norm) continue;
+            norm = true;
+            v = e;
+        } else {
+            fold_leaf_ivl(L[k], r, v, cnt);
+            norm = false;
+        }
+        CIvl R;
+        csg_c(ob.fold_op, acc, v, R, cnt);
+        acc = R;
+    }
+    return acc;
 }
 
 // Leaf Primitive::intersect without normal (t and acceptance only).
@@ -1012,7 +1156,8 @@ __device__ __forceinline__ DRay chain_ray(const DevScene& S, int pc0, int k, con
 // reference (ts, code) resolved later by resolve_hit().
 template <bool EAGER, bool DEEP, class CT>
 __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, const DRay& world, real tmin,
-                                           real tmax, real& t, V3& p, real& ts, int& code, CT& cnt) {
+                                           real tmax, real& t, V3& p, real& ts, int& code, CT& cnt,
+                                           uint64_t lmask = ~0ull, bool use_mask = false) {
     if (ob.kind <= rtamd::OBJ_POKE) {
         const bool ok = leaf_hit_t(&S.nodes[ob.node], world, tmin, tmax, t, cnt);
         p = ray_at(world, t);
@@ -1023,10 +1168,12 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
     if (ob.kind == rtamd::OBJ_CHAIN) {
         // transforms (transform.cpp): local ray, child on [0,inf), map back, project t
         DRay cur = world;
+        cnt.pb(PH_CHAIN_XF);
         for (int k = 0; k < ob.m; ++k) {
             cnt.inc(RT_OPC_XFORM);
             cur = local_ray(&S.nodes[S.ops[ob.pc0 + k].node], cur);
         }
+        cnt.pe(PH_CHAIN_XF);
         const real lo = ob.m ? RV(0.0) : tmin;
         const real hi = ob.m ? RT_INF : tmax;
         bool ok;
@@ -1036,13 +1183,15 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
             ts = t;
             code = ob.cpc0;
         } else {   // CSG::intersect (csg.cpp:169-185)
-            const CIvl R = run_compact<DEEP>(S, ob.cpc0, ob.cpc1, cur, cnt);
+            const CIvl R = (use_mask && ob.nfold > 0) ? run_fold(S, ob, cur, lmask, cnt)
+                                                      : run_compact<DEEP>(S, ob.cpc0, ob.cpc1, cur, cnt, lmask, use_mask);
             t = dmax(R.t0, lo);
             ok = R.ok && (t < R.t1 && t < hi);
             p = v3(cur.o.x + cur.d.x * t, cur.o.y + cur.d.y * t, cur.o.z + cur.d.z * t);
             ts = R.s0;
             code = R.c0;
         }
+        cnt.pb(PH_CHAIN_XF);
         for (int k = ob.m - 1; k >= 0; --k) {
             const DRay parent = (k == 0) ? world : chain_ray(S, ob.pc0, k, world);
             const NodeT* nd = &S.nodes[S.ops[ob.pc0 + k].node];
@@ -1053,6 +1202,7 @@ __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, 
             p = wp;
             t = wt;
         }
+        cnt.pe(PH_CHAIN_XF);
         return ok;
     }
     if constexpr (EAGER) {
@@ -1207,6 +1357,24 @@ __device__ __forceinline__ bool capsule_touch(const float* g, float ax, float ay
     return !(d2 > R * R);   // NaN passes
 }
 
+// The same bundle seen as LINES (Primitive::interval has no range, so a CSG
+// leaf's interval is empty only if its whole line misses the leaf): every
+// lane's line lies within rho of a line through (ox, oy, oz) whose direction
+// is within theta of +-a, so a ball can be touched only if the angle between
+// w = c - o and the axis LINE is <= theta + asin(R / |w|): the double cone,
+// cone_touch with |w.a|.  Conservative in f32 like cone_touch.
+__device__ __forceinline__ bool line_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
+                                          float az, float cth, float sth, float rho, float mag) {
+    const float wx = g[0] - ox, wy = g[1] - oy, wz = g[2] - oz;
+    const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
+    const float R = g[3] + rho + m;
+    const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
+    if (!(L2 > R * R)) return true;
+    const float wa = __builtin_fabsf(__builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az)));
+    const float rhs = cth * __builtin_sqrtf(L2 - R * R) - sth * R;
+    return !(wa + m < rhs);
+}
+
 template <class CT>
 __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
     for (int i = 0; i < n; ++i) cnt.inc(k);
@@ -1217,6 +1385,7 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
 template <bool EAGER, bool DEEP, class CT>
 __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
+    cnt.pb(PH_WAVE_SETUP);
     const FRay fr = to_fray(r);
     const float ftmin = (float)tmin, ftmax = (float)tmax;
     const float Ax = __builtin_fmaf(ftmin, fr.dx, fr.ox), Ay = __builtin_fmaf(ftmin, fr.dy, fr.oy),
@@ -1242,6 +1411,11 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
     const float mag = __builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
                       __builtin_fabsf(by) + __builtin_fabsf(bz) + rho + 1.0f;
     const int lane = __lane_id();
+    // line bundle for the CSG leaf masks, built on first use (cap only)
+    const float lox = rdlane_f(fr.ox, f), loy = rdlane_f(fr.oy, f), loz = rdlane_f(fr.oz, f);
+    const float lax = rdlane_f(fr.dx, f), lay = rdlane_f(fr.dy, f), laz = rdlane_f(fr.dz, f);
+    bool lb_ready = false;
+    float lrho = 0.0f, lcth = -1.0f, lsth = 1.0f, lmag = 0.0f;
     bool hit = false;
     for (int base = 0; base < S.n_objs; base += 64) {
         const int j = base + lane;
@@ -1267,6 +1441,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         // every object of the chunk is a candidate)
         const int nc = S.n_objs - base;
         uint64_t m = cap ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        cnt.pe(PH_WAVE_SETUP);
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             if (need) {
                 int skipped = 0;
@@ -1282,24 +1457,58 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
-            // CSG objects: no lane's segment reaches a leaf ball (DevObj::pb0)
-            if (cap && ob.npb > 0 &&
-                !__any(lane < ob.npb && capsule_touch(S.gb + 4 * (ob.pb0 + lane), ax, ay, az, ux, uy, uz, uu, rho, mag))) {
-                if (need) cnt.inc(RT_OPC_CULLED);
-                continue;
+            cnt.pb(PH_OBJ_PREF);
+            // CSG objects: no lane's segment reaches a leaf ball (DevObj::pb0);
+            // otherwise the leaves whose balls no querying lane's line meets
+            uint64_t lmask = ~0ull;
+            bool use_mask = false;
+            if (cap && ob.npb > 0) {
+                const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
+                const bool in = lane < ob.npb;
+                if (!__any(in && capsule_touch(g, ax, ay, az, ux, uy, uz, uu, rho, mag))) {
+                    if (need) cnt.inc(RT_OPC_CULLED);
+                    cnt.pe(PH_OBJ_PREF);
+                    continue;
+                }
+                if (!lb_ready) {
+                    // line bundle of the querying lanes (lane f's line as the axis)
+                    lb_ready = true;
+                    const float dxo = fr.ox - lox, dyo = fr.oy - loy, dzo = fr.oz - loz;
+                    const float do2 = need ? dxo * dxo + dyo * dyo + dzo * dzo : 0.0f;
+                    const float dc = need ? __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, lax, __builtin_fmaf(fr.dy, lay, fr.dz * laz)))
+                                          : 0.0f;
+                    lrho = __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(do2))));
+                    const float dcm = __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f;
+                    lcth = 1.0f - dcm;
+                    lsth = __builtin_sqrtf(__builtin_fmaxf(0.0f, 1.0f - lcth * lcth)) + 1e-6f;
+                    lmag = __builtin_fabsf(lox) + __builtin_fabsf(loy) + __builtin_fabsf(loz) + lrho + 1.0f;
+                }
+#ifdef RT_NO_LEAF_MASK
+                use_mask = false;
+#else
+                use_mask = lcth > 0.0f;
+#endif
+                if (use_mask) lmask = __ballot(in && line_touch(g, lox, loy, loz, lax, lay, laz, lcth, lsth, lrho, lmag));
             }
             if (S.cull && ob.has_bound) {   // per-lane segment test (f32, cheaper than an FP64 miss)
                 if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
                     if (need) cnt.inc(RT_OPC_CULLED);
+                    cnt.pe(PH_OBJ_PREF);
                     continue;
                 }
             }
+            cnt.pe(PH_OBJ_PREF);
+            const bool csg_obj = ob.kind == rtamd::OBJ_CHAIN && ob.core != 0;
+            if (csg_obj) cnt.pb(PH_SHADOW_CSG);
+            cnt.pb(PH_OBJ_HIT);
             if (need && !hit) {
                 real t = RV(0.0), ts = RV(0.0);
                 V3 p;
                 int code = 0;
-                hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
+                hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt, lmask, use_mask);
             }
+            cnt.pe(PH_OBJ_HIT);
+            if (csg_obj) cnt.pe(PH_SHADOW_CSG);
             if (__all(hit || !need)) return hit;
         }
     }
@@ -1332,6 +1541,7 @@ __device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, f
 template <bool EAGER, bool DEEP, class CT>
 __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin, real tmax, real& t_best,
                                      DHit& best, bool wave_ok, CT& cnt) {
+    cnt.pb(PH_WAVE_SETUP);
     const FRay fr = to_fray(r);
     const bool fin = __builtin_isfinite(fr.ox + fr.oy + fr.oz + fr.dx + fr.dy + fr.dz);
     // no cone for a partially active wave or non-finite rays: every object is
@@ -1365,6 +1575,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
         }
         const int nc = S.n_objs - base;
         uint64_t m = cone ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        cnt.pe(PH_WAVE_SETUP);
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             int skipped = 0;
             for (int o = base; o < S.n_objs && o < base + 64; ++o) {
@@ -1378,26 +1589,51 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
-            // CSG objects: the bundle reaches no leaf ball (DevObj::pb0)
-            if (!wide && ob.npb > 0 &&
-                !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + lane), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
+            cnt.pb(PH_OBJ_PREF);
+            // CSG objects: the bundle reaches no leaf ball (DevObj::pb0);
+            // otherwise the leaves whose balls no lane's line meets
+            uint64_t lmask = ~0ull;
+#ifdef RT_NO_LEAF_MASK
+            const bool use_mask = false;
+            if (!wide && ob.npb > 0 && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
                 cnt.inc(RT_OPC_CULLED);
+                cnt.pe(PH_OBJ_PREF);
                 continue;
+            }
+#else
+            const bool use_mask = !wide && ob.npb > 0;
+#endif
+            if (use_mask) {
+                const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
+                const bool in = lane < ob.npb;
+                if (!__any(in && cone_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
+                    cnt.inc(RT_OPC_CULLED);
+                    cnt.pe(PH_OBJ_PREF);
+                    continue;
+                }
+                lmask = __ballot(in && line_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
             }
             if (S.cull && ob.has_bound && !__any(ball_touch(ob.fb, fr, ftmin, (float)closest))) {
                 cnt.inc(RT_OPC_CULLED);
+                cnt.pe(PH_OBJ_PREF);
                 continue;
             }
+            cnt.pe(PH_OBJ_PREF);
             real t = RV(0.0), ts = RV(0.0);
             V3 p;
             int code = 0;
-            if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt)) {
+            const bool csg_obj = ob.kind == rtamd::OBJ_CHAIN && ob.core != 0;
+            if (csg_obj) cnt.pb(PH_PRIMARY_CSG);
+            cnt.pb(PH_OBJ_HIT);
+            if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt, lmask, use_mask)) {
                 closest = t;
                 win = o;
                 wp = p;
                 wts = ts;
                 wcode = code;
             }
+            cnt.pe(PH_OBJ_HIT);
+            if (csg_obj) cnt.pe(PH_PRIMARY_CSG);
         }
     }
     if (win < 0) return false;
@@ -1499,9 +1735,11 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
         }
         E = combine(E, combine(Ed, Es));
     }
+    if (WV) cnt.pb(PH_SHADE2);   // (pass 2 is timed from the end of pass 1; this start is overwritten)
     for (int l0 = 0; __any(valid) && l0 < S.n_lights; l0 += 32) {
         const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
         uint32_t lit = 0;
+        if (WV) cnt.pb(PH_SHADE1);
         for (int li = l0; li < l1; ++li) {
             const LightT* L = &S.lights[li];
             if (valid) cnt.inc(RT_OPC_LIGHT_EVAL);
@@ -1520,7 +1758,9 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             const DRay sr = make_ray(so, wi);
             bool occ = false;
             if constexpr (WV) {
+                cnt.pb(PH_SHADOW);
                 occ = scene_occluded_wave<EAGER, DEEP>(S, sr, eps, max_t, need, wave_full, cnt);
+                cnt.pe(PH_SHADOW);
             } else {
                 if (need) occ = scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt);
             }
@@ -1528,6 +1768,10 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 ++n_occl;
                 if (!occ) lit |= 1u << (li - l0);
             }
+        }
+        if (WV) {
+            cnt.pe(PH_SHADE1);
+            cnt.pb(PH_SHADE2);
         }
         if (!lit) continue;
         const MatT* m = &S.mats[hit.mat];
@@ -1561,6 +1805,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             E = combine(E, combine(Ed, Es));
         }
     }
+    if (WV) cnt.pe(PH_SHADE2);
     E.x = dmin(RV(1.5), E.x);
     E.y = dmin(RV(1.5), E.y);
     E.z = dmin(RV(1.5), E.z);
@@ -1590,8 +1835,10 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
         if constexpr (WV) {
             // miss lanes stay in shade() (valid = false) so that the wave
             // stays fully active for the wave-level shadow queries
+            cnt.pb(PH_PRIMARY);
             const bool hit = scene_intersect_wave<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h,
                                                                __builtin_amdgcn_read_exec() == ~0ull, cnt);
+            cnt.pe(PH_PRIMARY);
             if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);
             const V3 E = shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, hit);
             return hit ? E : v3(S.bg[0], S.bg[1], S.bg[2]);

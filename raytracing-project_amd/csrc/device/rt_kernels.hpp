@@ -30,7 +30,11 @@ namespace {
 // L2 (~6 ns each, MI355X_MICROARCH.md fan-in row) - 12 ms per 4K frame.
 template <bool C>
 __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
+#ifdef RT_PHASE_PROF
+    constexpr int NW = C ? 18 : 2 + PH_COUNT;
+#else
     constexpr int NW = C ? 18 : 2;
+#endif
     __shared__ unsigned long long red[4][NW];
     unsigned long long v[NW];
     v[0] = ni;
@@ -39,6 +43,12 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[2 + k] = cnt.c[k];
     }
+#ifdef RT_PHASE_PROF
+    if constexpr (!C) {
+#pragma unroll
+        for (int k = 0; k < PH_COUNT; ++k) v[2 + k] = (threadIdx.x & 63) == 0 ? cnt.get(k) : 0ull;
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < NW; ++k)
 #pragma unroll
@@ -75,15 +85,19 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     const bool active = x < P.W && ri < P.n_rows;
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
+    cnt.init();
     V3 c = v3(RV(0.0), RV(0.0), RV(0.0));
     if (active) {
+        cnt.pb(PH_SETUP);
         const int r = P.rows[ri];
         const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
         // draws 16p+2s, 16p+2s+1 of the stream: dx, dy (tracer.cpp:293)
         const double2 j = *reinterpret_cast<const double2*>(P.jit + ((size_t)P.jrow[ri] * P.W + x) * 16 + 2 * s);
         const DRay ray = gen_ray_subpixel(S, x, y, RV(j.x), RV(j.y));
+        cnt.pe(PH_SETUP);
         c = trace<E, D, SEC, DL, WV>(S, ray, ni, no, cnt);
     }
+    cnt.pb(PH_TAIL);
     // acc += trace(...) for s = 0..7 in order (tracer.cpp:290-296)
     const int base = lane & ~7;
     V3 acc = v3(RV(0.0), RV(0.0), RV(0.0));
@@ -103,6 +117,7 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
         o[1] = acc.y * inv;
         o[2] = acc.z * inv;
     }
+    cnt.pe(PH_TAIL);
     flush_counters(P.counters, ni, no, cnt);
 }
 
@@ -129,6 +144,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     const bool active = x < P.W && li < P.n_list;
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
+    cnt.init();
     if (active) {
         const int ei = P.ext_list[li];
         const int y = P.ext_rows[ei];
@@ -257,6 +273,7 @@ DevScene make_scene(const SceneView& V) {
     S.objs = V.objs;
     S.ops = V.ops;
     S.gb = V.gb;
+    S.fold = static_cast<const FoldT*>(V.fold);
     S.n_lights = V.n_lights;
     S.n_dlights = V.n_dlights;
     S.n_bounded = V.n_bounded;

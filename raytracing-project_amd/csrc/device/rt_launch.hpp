@@ -46,6 +46,14 @@ struct DLightR {
     T dir[3];
     T radiance[3];
 };
+template <class T>
+struct FoldLeafR {   // FoldLeaf (scene_compile.hpp) in the launching precision
+    T c[3];
+    T r;
+    int32_t pc;
+    int32_t pad;
+};
+static_assert(sizeof(FoldLeafR<double>) == sizeof(FoldLeaf), "FoldLeafR<double> must mirror FoldLeaf");
 static_assert(sizeof(NodeR<double>) == sizeof(rt_node), "NodeR<double> must mirror rt_node");
 static_assert(sizeof(MatR<double>) == sizeof(rt_material), "MatR<double> must mirror rt_material");
 static_assert(sizeof(LightR<double>) == sizeof(rt_light), "LightR<double> must mirror rt_light");
@@ -61,6 +69,7 @@ struct SceneView {
     const DevObj* objs;
     const DevOp* ops;
     const float* gb;
+    const void* fold;   // FoldLeafR of the launching precision
     int n_lights, n_dlights, n_objs;
     int n_bounded;
     int cam_nx, cam_ny;

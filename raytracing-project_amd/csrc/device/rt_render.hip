@@ -114,7 +114,8 @@ struct DBuf {
 struct Workspace {
     std::mutex mu;
     DBuf nodes, mats, lights, dlights, objs, ops, gb;
-    DBuf nodes_f, mats_f, lights_f, dlights_f;   // float copies (RT_FLAG_FP32)
+    DBuf fold;
+    DBuf nodes_f, mats_f, lights_f, dlights_f, fold_f;   // float copies (RT_FLAG_FP32)
     DBuf rows, jit, ckpt, jscratch, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
     std::map<int, rtamd::JitterPlan> jplan;   // per segment length K
@@ -176,6 +177,7 @@ struct rt_frame {
     std::vector<rtamd::MatR<float>> mats_f;
     std::vector<rtamd::LightR<float>> lights_f;
     std::vector<rtamd::DLightR<float>> dlights_f;
+    std::vector<rtamd::FoldLeafR<float>> fold_f;
 };
 
 namespace {
@@ -222,6 +224,13 @@ void make_float_scene(rt_frame& f) {
     for (size_t i = 0; i < f.dlights.size(); ++i) {
         to_float(f.dlights_f[i].dir, f.dlights[i].dir);
         to_float(f.dlights_f[i].radiance, f.dlights[i].radiance);
+    }
+    f.fold_f.resize(f.cs.fold.size());
+    for (size_t i = 0; i < f.cs.fold.size(); ++i) {
+        to_float(f.fold_f[i].c, f.cs.fold[i].c);
+        f.fold_f[i].r = (float)f.cs.fold[i].r;
+        f.fold_f[i].pc = f.cs.fold[i].pc;
+        f.fold_f[i].pad = 0;
     }
 }
 
@@ -301,11 +310,13 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(upload(ws.mats_f, f->mats_f, st));
         HIP_TRY(upload(ws.lights_f, f->lights_f, st));
         HIP_TRY(upload(ws.dlights_f, f->dlights_f, st));
+        HIP_TRY(upload(ws.fold_f, f->fold_f, st));
     } else {
         HIP_TRY(upload(ws.nodes, f->nodes, st));
         HIP_TRY(upload(ws.mats, f->mats, st));
         HIP_TRY(upload(ws.lights, f->lights, st));
         HIP_TRY(upload(ws.dlights, f->dlights, st));
+        HIP_TRY(upload(ws.fold, f->cs.fold, st));
     }
     HIP_TRY(upload(ws.objs, f->cs.objs, st));
     HIP_TRY(upload(ws.ops, f->cs.ops, st));
@@ -319,6 +330,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.mats = f->fp32 ? ws.mats_f.p : ws.mats.p;
     S.lights = f->fp32 ? ws.lights_f.p : ws.lights.p;
     S.dlights = f->fp32 ? ws.dlights_f.p : ws.dlights.p;
+    S.fold = f->fp32 ? ws.fold_f.p : ws.fold.p;
     S.n_dlights = d.n_dir_lights;
     S.objs = ws.objs.as<rtamd::DevObj>();
     S.ops = ws.ops.as<rtamd::DevOp>();

@@ -120,6 +120,49 @@ public:
         cs.gbounds.insert(cs.gbounds.end(), balls.begin(), balls.end());
     }
 
+    // A compact CSG core that is a left-deep fold of ONE operator whose
+    // operands are all sphere / pokeball leaves (the loader's n-ary
+    // union / intersection / difference arrays, json_loader.cpp:375-401, and
+    // binary csg chains of that shape) gets a flat leaf table: the device
+    // evaluates it as acc = leaf_0; acc = acc op leaf_k (csg.cpp:61-163)
+    // without the op interpreter, skipping leaves by the wave's line mask
+    // (rt_device.hpp run_fold).  Needs the leaf prefilter balls (same order).
+    void fold_leaves(DevObj& o, int core, CompiledScene& cs) {
+        if (o.npb <= 0) return;
+        const int op = d_.nodes[core].op;
+        std::vector<int> rhs;
+        int cur = core;
+        while (d_.nodes[cur].kind == RT_NODE_CSG && d_.nodes[cur].op == op) {
+            rhs.push_back(d_.nodes[cur].b);
+            cur = d_.nodes[cur].a;
+        }
+        auto is_ball = [&](int i) {
+            const int k = d_.nodes[i].kind;
+            return k == RT_NODE_SPHERE || k == RT_NODE_POKEBALL;
+        };
+        if (!is_ball(cur)) return;
+        for (int b : rhs)
+            if (!is_ball(b)) return;
+        std::vector<int> leaves{cur};
+        for (size_t k = rhs.size(); k-- > 0;) leaves.push_back(rhs[k]);   // innermost first
+        std::vector<int> pcs;
+        for (int pc = o.cpc0; pc < o.cpc1; ++pc)
+            if (cs.ops[pc].op == OP_LEAF_IVL) pcs.push_back(pc);
+        if (pcs.size() != leaves.size() || (int)leaves.size() != o.npb || leaves.size() > 64) return;
+        o.fold0 = (int)cs.fold.size();
+        o.nfold = (int)leaves.size();
+        o.fold_op = op;
+        for (size_t k = 0; k < leaves.size(); ++k) {
+            const rt_node& n = d_.nodes[leaves[k]];
+            if (cs.ops[pcs[k]].node != leaves[k]) throw std::runtime_error("fold leaf order mismatch");
+            FoldLeaf f{};
+            for (int i = 0; i < 3; ++i) f.c[i] = n.v[i];
+            f.r = n.v[3];
+            f.pc = pcs[k];
+            cs.fold.push_back(f);
+        }
+    }
+
     Bound bound(int idx, int level = 0) {
         if (level > 4096) throw std::runtime_error("scene graph too deep");
         const rt_node& n = d_.nodes[idx];
@@ -374,7 +417,10 @@ public:
                 }
                 o.cpc1 = (int)cs.ops.size();
                 o.pc1 = o.cpc1;
-                if (!leaf_core) leaf_prefilter(o, chain, core, cs);
+                if (!leaf_core) {
+                    leaf_prefilter(o, chain, core, cs);
+                    fold_leaves(o, core, cs);
+                }
             } else {
                 o.kind = OBJ_EAGER;
                 cs.has_eager = true;

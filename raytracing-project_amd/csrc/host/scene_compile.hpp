@@ -57,10 +57,23 @@ struct DevObj {
     int32_t has_bound;  // conservative world-space bounding sphere present
     int32_t pb0;        // CHAIN with a compact CSG core: first leaf prefilter ball in gbounds (units of 4 floats)
     int32_t npb;        //   and their count (0 = none): world balls of every leaf, grown by the CSG epsilon slop
+    int32_t fold0;      // CHAIN whose CSG core is a left-deep fold of one operator over sphere / pokeball
+    int32_t nfold;      //   leaves (the loader's n-ary arrays): first FoldLeaf and leaf count (0 = not a fold)
+    int32_t fold_op;    //   the fold's rt_csg_op
     int32_t pad;
     double bc[3];       // bound centre
     double br;          // bound radius (already inflated)
     float fb[4];        // the same ball in float (cx, cy, cz, r), inflated for the f32 cull test
+};
+
+// One leaf of a fold object (DevObj::fold0), in fold order = the order of the
+// object's OP_LEAF_IVL ops and of its prefilter balls.  pc is the leaf's
+// OP_LEAF_IVL op index (its lazy hit-reference code).
+struct FoldLeaf {
+    double c[3];
+    double r;
+    int32_t pc;
+    int32_t pad;
 };
 
 struct DevOp {
@@ -73,6 +86,7 @@ struct DevOp {
 struct CompiledScene {
     std::vector<DevObj> objs;
     std::vector<DevOp> ops;
+    std::vector<FoldLeaf> fold;    // leaves of the fold objects (DevObj::fold0)
     std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated;
                                    // then the leaf prefilter balls of CHAIN objects (world frame, see DevObj::pb0)
     int max_ray_depth = 0;   // transform nesting on any path
