@@ -12,6 +12,11 @@
  *                               raytracer/src/json_loader.cpp:499-503
  *   rt_render                <- Tracer::render (standard + paper mode)
  *                               raytracer/src/tracer.cpp:247-305, tracer.h:18-35
+ *   rt_render_multi          <- Tracer::render over the GPUs of one node (row
+ *                               strips + RCCL gather)
+ *   rt_render_rgb8           <- Tracer::render + framebuffer_to_mat_bgr8
+ *                               (main.cpp:19-34, 74-89) on the device
+ *   rt_dist_* / rt_render_dist <- the same for one process per GPU
  *   rt_render_rows_device    <- the same loop restricted to a set of output
  *                               rows (multi-GPU row tiling)
  *   rt_frame_begin/trace/end <- the same loop, split so that row chunks can
@@ -40,7 +45,10 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2   /* 2: rt_scene_desc gained directional lights */
+#define RT_ABI_VERSION 3   /* 2: rt_scene_desc gained directional lights
+                              3: rt_stats gained the output-path timings; multi-GPU
+                                 and device-output entry points (rt_render_multi,
+                                 rt_render_rgb8, rt_dist_*) */
 
 /* ---------------------------------------------------------------- errors */
 enum rt_status {
@@ -181,6 +189,12 @@ typedef struct rt_stats {
     double ms_kernel;          /* trace kernels (device)                                        */
     double ms_total;           /* whole call, host wall clock                                   */
     uint64_t ops[16];          /* per-op counters when RT_FLAG_COUNT_OPS is set (rt_op_counter) */
+    /* ABI 3: the rest of the frame's wall clock */
+    double ms_gather;          /* multi-GPU: RCCL gather of the row strips + placement on the root (device) */
+    double ms_tobyte;          /* device toByte + RGB packing (rt_render_rgb8)                      */
+    double ms_d2h;             /* device -> host copy of the result                                 */
+    int32_t n_gpus;            /* devices that rendered                                             */
+    int32_t pad_;
 } rt_stats;
 
 /* Op counters used by the FLOP model. */
@@ -219,6 +233,46 @@ enum rt_flags {
  * Uses the current HIP device; blocks until done. */
 int rt_render(const rt_scene* s, int W, int H, int mode, int flags,
               double* fb_host, rt_stats* stats);
+
+/* Tracer::render over n_gpus HIP devices of THIS process (n_gpus <= 0: all
+ * visible devices): every device renders interleaved strips of RT_STRIP_ROWS
+ * output rows (strip s -> device s mod n, rt_dist_rows), and the strips reach
+ * device 0 through RCCL ncclGather over xGMI (one collective per row chunk,
+ * overlapped with the tracing of the next chunk) before the one D2H copy into
+ * fb_host.  The result is bit-identical to rt_render (same kernels, same
+ * jitter-stream offsets).  n_gpus == 1 is rt_render. */
+int rt_render_multi(const rt_scene* s, int W, int H, int mode, int flags, int n_gpus, double* fb_host,
+                    rt_stats* stats);
+
+/* Tracer::render followed by framebuffer_to_mat_bgr8's toByte
+ * (main.cpp:19-34, core.h:313-316) on the device(s), RGB order, top row
+ * first: only 3 bytes per pixel cross xGMI and PCIe.
+ * This is the CLI's path (`ray ... --gpus N`). */
+int rt_render_rgb8(const rt_scene* s, int W, int H, int mode, int flags, int n_gpus, uint8_t* rgb8_host,
+                   rt_stats* stats);
+
+/* ------------------------------------------- one process per GPU (RCCL)
+ * For launchers that start one process per device (torchrun, MPI): rank 0
+ * calls rt_dist_get_id and hands the RT_DIST_ID_BYTES bytes to every rank,
+ * each rank binds its current HIP device with rt_dist_create, and every
+ * frame each rank calls rt_render_dist[_rgb8]: it renders its strips
+ * (rt_dist_rows) and rank 0 receives the whole frame in its device buffer
+ * (the ncclGather of rt_render_multi).  Non-root ranks pass NULL.  The call
+ * returns when this rank's part (and on rank 0 the whole frame) is done;
+ * stats are this rank's (ray counts of its rows). */
+#define RT_STRIP_ROWS 8
+#define RT_DIST_ID_BYTES 128
+typedef struct rt_dist rt_dist;
+int rt_dist_get_id(uint8_t id[RT_DIST_ID_BYTES]);
+int rt_dist_create(const uint8_t id[RT_DIST_ID_BYTES], int world, int rank, rt_dist** out);
+void rt_dist_destroy(rt_dist* d);
+int rt_render_dist(rt_dist* d, const rt_scene* s, int W, int H, int mode, int flags, double* fb_root_dev,
+                   void* hip_stream, rt_stats* stats);
+int rt_render_dist_rgb8(rt_dist* d, const rt_scene* s, int W, int H, int mode, int flags, uint8_t* rgb8_root_dev,
+                        void* hip_stream, rt_stats* stats);
+/* The partition: writes the output rows of `rank` (ascending) to rows_out
+ * (room for H entries) and returns their count; <0 on bad arguments. */
+int rt_dist_rows(int H, int world, int rank, int32_t* rows_out);
 
 /* Render an arbitrary set of OUTPUT rows (top-row-first indices) into a
  * compact device buffer fb_rows_dev[n_rows][W][3] on the given HIP stream

@@ -31,6 +31,15 @@ int rt_test_jitter_device(int K_blocks, int64_t q0, int64_t q1, int64_t first, i
 struct rt_scene;
 int rt_test_compile_info(const struct rt_scene* s, int32_t* out);
 
+/* GPU, one device: the multi-GPU frame path of rt_render_multi /
+ * rt_render_dist (partition, row chunks, gather stage layout, placement on
+ * the root) with `world` simulated ranks rendered one after another on the
+ * current device and the RCCL gather replaced by device copies into the same
+ * stage.  Writes the root's frame to fb_host (W*H*3 doubles) or, with rgb8,
+ * its bytes to rgb8_host.  For tests on one-GPU machines. */
+int rt_test_render_dist_sim(const struct rt_scene* s, int W, int H, int mode, int flags, int world, int rgb8,
+                            double* fb_host, uint8_t* rgb8_host);
+
 #ifdef __cplusplus
 }
 #endif

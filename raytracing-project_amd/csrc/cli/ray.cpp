@@ -4,12 +4,17 @@
 // (paper mode iff argv[3] == "--paper"), same exit codes
 // (1 usage, 2 load returned false, 3 exception while loading, 4 PNG write
 // failure) and the same final "Wrote <out> (WxH)[ (paper mode)]" line.
+// The frame is rendered, converted with toByte and packed on the GPU(s)
+// (rt_render_rgb8): 3 bytes per pixel reach the host,
+// then the PNG is deflated in parallel bands (rt_write_png).
 // Extra options may follow argv[3] (the reference ignores them):
-//   --stats        print one JSON line with ray counts and timings
+//   --gpus N       render on N GPUs of this node (row strips + RCCL gather); 0 = all
+//   --stats        print one JSON line with ray counts and the wall-clock split
 //   --threads N    deflate threads for the PNG writer (default 8)
 //   --fp32         NON-PARITY FP32 fast path (RT_FLAG_FP32)
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <string>
@@ -19,6 +24,7 @@
 #include "tracer.hpp"
 
 int main(int argc, char** argv) {
+    const auto t_start = std::chrono::steady_clock::now();
     if (argc < 3) {
         std::cerr << "Usage: " << argv[0] << " <scene.json> <output.png> [--paper]\n";
         std::cerr << "  --paper: Enable paper rendering mode with crosshatching\n";
@@ -30,11 +36,13 @@ int main(int argc, char** argv) {
     if (argc > 3 && std::string(argv[3]) == "--paper") paper_mode = true;
     bool print_stats = false;
     int png_threads = 8;
+    int n_gpus = 1;
     bool fp32 = false;
     for (int i = 3; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--stats")) print_stats = true;
         else if (!std::strcmp(argv[i], "--fp32")) fp32 = true;
         else if (!std::strcmp(argv[i], "--threads") && i + 1 < argc) png_threads = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) n_gpus = std::atoi(argv[++i]);
     }
 
     rtamd::Scene scene;
@@ -48,6 +56,7 @@ int main(int argc, char** argv) {
         std::cerr << "[error] " << e.what() << "\n";
         return 3;
     }
+    const auto t_loaded = std::chrono::steady_clock::now();
 
     const int W = cam.nx();
     const int H = cam.ny();
@@ -57,14 +66,15 @@ int main(int argc, char** argv) {
     tracer.width = W;
     tracer.height = H;
     tracer.mode = paper_mode ? rtamd::RenderMode::Paper : rtamd::RenderMode::Standard;
+    tracer.n_gpus = n_gpus;
     if (fp32) tracer.flags |= RT_FLAG_FP32;
 
     if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";
-    std::vector<rtamd::Color> framebuffer;
+    std::vector<uint8_t> rgb;
     const auto t0 = std::chrono::steady_clock::now();
     try {
-        tracer.render(framebuffer);
+        tracer.render_rgb8(rgb);
     } catch (const std::exception& e) {
         std::cerr << "[error] " << e.what() << "\n";
         return 5;
@@ -72,28 +82,25 @@ int main(int argc, char** argv) {
     const auto t1 = std::chrono::steady_clock::now();
     std::cout << "Rendering complete!\n";
 
-    std::vector<uint8_t> rgb((size_t)W * H * 3);
-    rt_framebuffer_to_rgb8(reinterpret_cast<const double*>(framebuffer.data()), (size_t)W * H, rgb.data());
-    const auto t2 = std::chrono::steady_clock::now();
     if (rt_write_png(out_path.c_str(), rgb.data(), W, H, png_threads) != RT_OK) {
         std::cerr << "Failed to write PNG: " << out_path << "\n";
         return 4;
     }
-    const auto t3 = std::chrono::steady_clock::now();
+    const auto t2 = std::chrono::steady_clock::now();
     std::string mode_str = paper_mode ? " (paper mode)" : "";
     std::cout << "Wrote " << out_path << " (" << W << "x" << H << ")" << mode_str << "\n";
     if (print_stats) {
         const rt_stats& s = tracer.stats;
-        const double ms_render = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        const double ms_png = std::chrono::duration<double, std::milli>(t3 - t1).count();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        const double ms_render = ms(t0, t1);
         const double rays = (double)(s.rays_intersect + s.rays_occluded);
         std::printf(
-            "{\"rays_intersect\": %llu, \"rays_occluded\": %llu, \"rays_traced\": %llu, \"ms_rng\": %.3f, "
-            "\"ms_kernel\": %.3f, \"ms_render\": %.3f, \"ms_png\": %.3f, \"mrays_per_s\": %.3f}\n",
+            "{\"rays_intersect\": %llu, \"rays_occluded\": %llu, \"rays_traced\": %llu, \"n_gpus\": %d, "
+            "\"ms_load\": %.3f, \"ms_rng\": %.3f, \"ms_kernel\": %.3f, \"ms_gather\": %.3f, \"ms_tobyte\": %.3f, "
+            "\"ms_d2h\": %.3f, \"ms_render\": %.3f, \"ms_png\": %.3f, \"ms_main\": %.3f, \"mrays_per_s\": %.3f}\n",
             (unsigned long long)s.rays_intersect, (unsigned long long)s.rays_occluded,
-            (unsigned long long)s.rays_traced, s.ms_rng, s.ms_kernel, ms_render, ms_png,
-            rays / (ms_render * 1e3));
-        (void)t2;
+            (unsigned long long)s.rays_traced, s.n_gpus, ms(t_start, t_loaded), s.ms_rng, s.ms_kernel, s.ms_gather,
+            s.ms_tobyte, s.ms_d2h, ms_render, ms(t1, t2), ms(t_start, t2), rays / (ms_render * 1e3));
     }
     return 0;
 }

@@ -6,6 +6,7 @@
 // Camera exposes ScreenSpec::nx()/ny() (camera.h:19-21).
 #pragma once
 
+#include <cstdint>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -73,6 +74,7 @@ struct Tracer {
     int height{360};
     RenderMode mode{RenderMode::Standard};
     int flags{RT_FLAG_NONE};
+    int n_gpus{1};                 // devices of this process (rt_render_multi); 0 = all visible
     mutable rt_stats stats{};
 
     // Tracer::render (tracer.cpp:247-305): returns silently when the scene or
@@ -81,8 +83,20 @@ struct Tracer {
     void render(std::vector<Color>& framebuffer) const {
         if (!scene || !scene->get() || !camera || width <= 0 || height <= 0) return;
         framebuffer.assign((size_t)width * height, Color{});
-        int rc = rt_render(scene->get(), width, height, mode == RenderMode::Paper ? RT_MODE_PAPER : RT_MODE_STANDARD,
-                           flags, reinterpret_cast<double*>(framebuffer.data()), &stats);
+        int rc = rt_render_multi(scene->get(), width, height,
+                                 mode == RenderMode::Paper ? RT_MODE_PAPER : RT_MODE_STANDARD, flags, n_gpus,
+                                 reinterpret_cast<double*>(framebuffer.data()), &stats);
+        if (rc != RT_OK) throw std::runtime_error(std::string("rt_render failed: ") + rt_last_error());
+    }
+
+    // render() + framebuffer_to_mat_bgr8's toByte (main.cpp:19-34) on the
+    // device: rgb[(y*W + x)*3 + c], RGB order, top row first.
+    void render_rgb8(std::vector<uint8_t>& rgb) const {
+        if (!scene || !scene->get() || !camera || width <= 0 || height <= 0) return;
+        rgb.assign((size_t)width * height * 3, 0);
+        int rc = rt_render_rgb8(scene->get(), width, height,
+                                mode == RenderMode::Paper ? RT_MODE_PAPER : RT_MODE_STANDARD, flags, n_gpus,
+                                rgb.data(), &stats);
         if (rc != RT_OK) throw std::runtime_error(std::string("rt_render failed: ") + rt_last_error());
     }
 };

@@ -110,6 +110,26 @@ struct DBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// The device-resident copy of one scene (compiled object table + records in
+// the launching precision).  A scene handle is immutable, so the copy is
+// keyed by its process-unique id and reused by every later frame of that
+// scene on the device: the inputs stay resident in HBM between frames.
+struct SceneCache {
+    bool valid = false;
+    uint64_t uid = 0;
+    bool fp32 = false;
+    rtamd::CompiledScene cs;
+    std::vector<rt_node> nodes;   // host sources of the uploads (kept alive)
+    std::vector<rt_material> mats;
+    std::vector<rt_light> lights;
+    std::vector<rt_dir_light> dlights;
+    std::vector<rtamd::NodeR<float>> nodes_f;
+    std::vector<rtamd::MatR<float>> mats_f;
+    std::vector<rtamd::LightR<float>> lights_f;
+    std::vector<rtamd::DLightR<float>> dlights_f;
+    std::vector<rtamd::FoldLeafR<float>> fold_f;
+};
+
 // Per-device workspace (one render at a time per device; guarded by a mutex).
 struct Workspace {
     std::mutex mu;
@@ -123,6 +143,7 @@ struct Workspace {
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
+    SceneCache sc;
 };
 
 Workspace& workspace(int dev) {
@@ -168,16 +189,6 @@ struct rt_frame {
     int n_tev = 0;                             // trace events recorded (ws.tev[0 .. n_tev))
     hipStream_t last_st = nullptr;             // stream of the previous trace call
     std::vector<std::vector<int32_t>> stage;   // host sources of async uploads
-    rtamd::CompiledScene cs;
-    std::vector<rt_node> nodes;
-    std::vector<rt_material> mats;
-    std::vector<rt_light> lights;
-    std::vector<rt_dir_light> dlights;
-    std::vector<rtamd::NodeR<float>> nodes_f;
-    std::vector<rtamd::MatR<float>> mats_f;
-    std::vector<rtamd::LightR<float>> lights_f;
-    std::vector<rtamd::DLightR<float>> dlights_f;
-    std::vector<rtamd::FoldLeafR<float>> fold_f;
 };
 
 namespace {
@@ -188,7 +199,7 @@ void to_float(float (&dst)[N], const double (&src)[N]) {
 }
 
 // Float copies of the scene records for the FP32 kernels (RT_FLAG_FP32).
-void make_float_scene(rt_frame& f) {
+void make_float_scene(SceneCache& f) {
     f.nodes_f.resize(f.nodes.size());
     for (size_t i = 0; i < f.nodes.size(); ++i) {
         const rt_node& s = f.nodes[i];
@@ -256,13 +267,49 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         return RT_ERR_NO_DEVICE;
     }
     const rt_scene_desc& d = *rt_scene_get_desc(s);
-    rtamd::CompiledScene cs;
-    try {
-        cs = rtamd::compile_scene(d);
-    } catch (const std::exception& e) {
-        rtamd::set_last_error(std::string("scene compile: ") + e.what());
-        return RT_ERR_INVALID_ARG;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::unique_ptr<rt_frame> f(new rt_frame);
+    f->ws = &workspace(dev);
+    f->lock = std::unique_lock<std::mutex>(f->ws->mu);
+    Workspace& ws = *f->ws;
+    const bool fp32 = (flags & RT_FLAG_FP32) != 0;
+    SceneCache& sc = ws.sc;
+    if (!sc.valid || sc.uid != rtamd::scene_uid(s) || sc.fp32 != fp32) {
+        // compile + upload the scene once; later frames of it find it resident
+        sc.valid = false;
+        try {
+            sc.cs = rtamd::compile_scene(d);
+        } catch (const std::exception& e) {
+            rtamd::set_last_error(std::string("scene compile: ") + e.what());
+            return RT_ERR_INVALID_ARG;
+        }
+        sc.nodes.assign(d.nodes, d.nodes + d.n_nodes);
+        sc.mats.assign(d.materials, d.materials + d.n_materials);
+        sc.lights.assign(d.lights, d.lights + d.n_lights);
+        sc.dlights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
+        if (fp32) {
+            make_float_scene(sc);
+            HIP_TRY(upload(ws.nodes_f, sc.nodes_f, st));
+            HIP_TRY(upload(ws.mats_f, sc.mats_f, st));
+            HIP_TRY(upload(ws.lights_f, sc.lights_f, st));
+            HIP_TRY(upload(ws.dlights_f, sc.dlights_f, st));
+            HIP_TRY(upload(ws.fold_f, sc.fold_f, st));
+        } else {
+            HIP_TRY(upload(ws.nodes, sc.nodes, st));
+            HIP_TRY(upload(ws.mats, sc.mats, st));
+            HIP_TRY(upload(ws.lights, sc.lights, st));
+            HIP_TRY(upload(ws.dlights, sc.dlights, st));
+            HIP_TRY(upload(ws.fold, sc.cs.fold, st));
+        }
+        HIP_TRY(upload(ws.objs, sc.cs.objs, st));
+        HIP_TRY(upload(ws.ops, sc.cs.ops, st));
+        HIP_TRY(upload(ws.gb, sc.cs.gbounds, st));
+        sc.uid = rtamd::scene_uid(s);
+        sc.fp32 = fp32;
+        sc.valid = true;
     }
+    const rtamd::CompiledScene& cs = sc.cs;
     if (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2) {
         rtamd::set_last_error("scene nesting exceeds the device stacks (transforms <= 8, CSG operand depth <= 8)");
         return RT_ERR_UNSUPPORTED;
@@ -275,12 +322,6 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         rtamd::set_last_error("medium.recursion exceeds the device frame stack (17)");
         return RT_ERR_UNSUPPORTED;
     }
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    std::unique_ptr<rt_frame> f(new rt_frame);
-    f->ws = &workspace(dev);
-    f->lock = std::unique_lock<std::mutex>(f->ws->mu);
-    Workspace& ws = *f->ws;
     f->st = st;
     f->W = W;
     f->H = H;
@@ -292,53 +333,29 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->deep = cs.max_ivl_depth > 2 || d.n_dir_lights > 0;
     f->secondary = secondary;
     f->count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
-    f->fp32 = (flags & RT_FLAG_FP32) != 0;
+    f->fp32 = fp32;
     f->rows.assign(rows_host, rows_host + n_rows);
     f->t_start = t_start;
     if (!ws.ev[0])
         for (int i = 0; i < 4; ++i) HIP_TRY(hipEventCreate(&ws.ev[i]));
-
-    // --- upload the scene (a few KB; the frame keeps the host copies alive)
-    f->nodes.assign(d.nodes, d.nodes + d.n_nodes);
-    f->mats.assign(d.materials, d.materials + d.n_materials);
-    f->lights.assign(d.lights, d.lights + d.n_lights);
-    f->dlights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
-    f->cs = std::move(cs);
-    if (f->fp32) {
-        make_float_scene(*f);
-        HIP_TRY(upload(ws.nodes_f, f->nodes_f, st));
-        HIP_TRY(upload(ws.mats_f, f->mats_f, st));
-        HIP_TRY(upload(ws.lights_f, f->lights_f, st));
-        HIP_TRY(upload(ws.dlights_f, f->dlights_f, st));
-        HIP_TRY(upload(ws.fold_f, f->fold_f, st));
-    } else {
-        HIP_TRY(upload(ws.nodes, f->nodes, st));
-        HIP_TRY(upload(ws.mats, f->mats, st));
-        HIP_TRY(upload(ws.lights, f->lights, st));
-        HIP_TRY(upload(ws.dlights, f->dlights, st));
-        HIP_TRY(upload(ws.fold, f->cs.fold, st));
-    }
-    HIP_TRY(upload(ws.objs, f->cs.objs, st));
-    HIP_TRY(upload(ws.ops, f->cs.ops, st));
-    HIP_TRY(upload(ws.gb, f->cs.gbounds, st));
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
 
     SceneView& S = f->S;
-    S.nodes = f->fp32 ? ws.nodes_f.p : ws.nodes.p;
-    S.mats = f->fp32 ? ws.mats_f.p : ws.mats.p;
-    S.lights = f->fp32 ? ws.lights_f.p : ws.lights.p;
-    S.dlights = f->fp32 ? ws.dlights_f.p : ws.dlights.p;
-    S.fold = f->fp32 ? ws.fold_f.p : ws.fold.p;
+    S.nodes = fp32 ? ws.nodes_f.p : ws.nodes.p;
+    S.mats = fp32 ? ws.mats_f.p : ws.mats.p;
+    S.lights = fp32 ? ws.lights_f.p : ws.lights.p;
+    S.dlights = fp32 ? ws.dlights_f.p : ws.dlights.p;
+    S.fold = fp32 ? ws.fold_f.p : ws.fold.p;
     S.n_dlights = d.n_dir_lights;
     S.objs = ws.objs.as<rtamd::DevObj>();
     S.ops = ws.ops.as<rtamd::DevOp>();
     S.gb = ws.gb.as<float>();
     S.n_lights = d.n_lights;
-    S.n_objs = (int)f->cs.objs.size();
+    S.n_objs = (int)cs.objs.size();
     S.n_bounded = 0;
-    for (const auto& o : f->cs.objs)
+    for (const auto& o : cs.objs)
         if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++S.n_bounded;
     S.cam_nx = rt_camera_width(&d.camera);
     S.cam_ny = rt_camera_height(&d.camera);
@@ -562,6 +579,7 @@ int frame_end(rt_frame* f, rt_stats* stats) {
         for (int k = 0; k < 16; ++k) stats->ops[k] = hc[2 + k];
         stats->ms_total =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f->t_start).count();
+        stats->n_gpus = 1;
     }
     return RT_OK;
 }
@@ -622,9 +640,13 @@ extern "C" int rt_render(const rt_scene* s, int W, int H, int mode, int flags, d
     HIP_TRY(fb.ensure(bytes));
     int rc = render_rows_impl(s, W, H, mode, flags, rows.data(), H, fb.as<double>(), nullptr, stats);
     if (rc != RT_OK) return rc;
+    const auto t1 = std::chrono::steady_clock::now();
     HIP_TRY(hipMemcpy(fb_host, fb.p, bytes, hipMemcpyDeviceToHost));
-    if (stats)
-        stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) {
+        const auto t2 = std::chrono::steady_clock::now();
+        stats->ms_d2h = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        stats->ms_total = std::chrono::duration<double, std::milli>(t2 - t0).count();
+    }
     return RT_OK;
 }
 

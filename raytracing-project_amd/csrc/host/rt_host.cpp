@@ -1,6 +1,7 @@
 // rt_host.cpp — C-ABI entry points of librt_host.so (scene loading and IR
 // access).  No exceptions cross the ABI: failures return an rt_status and
 // leave the message in rt_last_error().
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -32,13 +33,18 @@ extern "C" int rt_camera_height(const rt_camera* c) {  // camera.h:21
     return n > 1 ? n : 1;
 }
 
+static std::atomic<uint64_t> g_next_uid{1};
+
 static rt_scene* wrap(rtamd::SceneIR&& ir) {
     rt_scene* s = new (std::nothrow) rt_scene;
     if (!s) return nullptr;
     s->ir = std::move(ir);
     s->d = s->ir.desc();
+    s->uid = g_next_uid.fetch_add(1);
     return s;
 }
+
+uint64_t rtamd::scene_uid(const rt_scene* s) { return s ? s->uid : 0; }
 
 static int classify(const std::string& msg) {
     if (msg.rfind("JSON parse error: ", 0) == 0) return RT_ERR_PARSE;

@@ -1,6 +1,7 @@
 // rt_internal.hpp — helpers shared between librt_host and librtamd.
 #pragma once
 
+#include <cstdint>
 #include <string>
 
 #include "rt.h"
@@ -10,4 +11,7 @@ void set_last_error(const std::string& msg);
 void clear_last_error();
 bool validate_desc(const rt_scene_desc& d, std::string* why);
 bool node_depth_ok(const rt_scene_desc& d, int idx, int level, int* maxdepth);
+// Process-unique id of a scene handle (scenes are immutable after creation,
+// so a device copy keyed by it never goes stale).
+uint64_t scene_uid(const rt_scene* s);
 }  // namespace rtamd

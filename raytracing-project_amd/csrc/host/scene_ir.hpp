@@ -56,4 +56,5 @@ SceneIR load_scene_from_json_file(const std::string& path);
 struct rt_scene {
     rtamd::SceneIR ir;
     rt_scene_desc d;
+    uint64_t uid = 0;   // process-unique, never reused: keys the device-resident copies (rt_render.hip)
 };

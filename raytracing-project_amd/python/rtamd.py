@@ -86,7 +86,9 @@ class SceneDesc(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("rays_intersect", C.c_uint64), ("rays_occluded", C.c_uint64), ("rays_traced", C.c_uint64),
                 ("pixels", C.c_uint64), ("ms_rng", C.c_double), ("ms_kernel", C.c_double),
-                ("ms_total", C.c_double), ("ops", C.c_uint64 * 16)]
+                ("ms_total", C.c_double), ("ops", C.c_uint64 * 16),
+                ("ms_gather", C.c_double), ("ms_tobyte", C.c_double), ("ms_d2h", C.c_double),
+                ("n_gpus", C.c_int32), ("pad_", C.c_int32)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ops"}
@@ -159,6 +161,21 @@ def amd_lib():
             lib.rt_frame_end.argtypes = [C.c_void_p, C.POINTER(Stats)]
         lib.rt_framebuffer_to_rgb8_device.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]
         lib.rt_device_count.restype = C.c_int
+        lib.rt_render_multi.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp,
+                                        C.POINTER(Stats)]
+        lib.rt_render_rgb8.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(C.c_uint8), C.POINTER(Stats)]
+        lib.rt_dist_get_id.argtypes = [C.POINTER(C.c_uint8)]
+        lib.rt_dist_create.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+        lib.rt_dist_destroy.argtypes = [C.c_void_p]
+        lib.rt_dist_destroy.restype = None
+        lib.rt_render_dist.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                       C.c_void_p, C.POINTER(Stats)]
+        lib.rt_render_dist_rgb8.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.POINTER(Stats)]
+        lib.rt_dist_rows.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32)]
+        lib.rt_test_render_dist_sim.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                _dp, C.POINTER(C.c_uint8)]
         _amd = lib
     return _amd
 
@@ -317,6 +334,57 @@ class Tracer:
         if rc != RT_OK:
             raise RTError(rc, last_error())
         return fb
+
+
+def render_multi(scene: Scene, width: int, height: int, mode: int, n_gpus: int, flags: int = RT_FLAG_NONE,
+                 stats: Stats | None = None) -> np.ndarray:
+    """rt_render_multi: the frame over n_gpus devices of this process."""
+    fb = np.zeros((height, width, 3), dtype=np.float64)
+    st = stats if stats is not None else Stats()
+    rc = amd_lib().rt_render_multi(scene.handle, width, height, mode, flags, n_gpus, fb.ctypes.data_as(_dp),
+                                   C.byref(st))
+    if rc != RT_OK:
+        raise RTError(rc, last_error())
+    return fb
+
+
+def render_rgb8(scene: Scene, width: int, height: int, mode: int, n_gpus: int = 1, flags: int = RT_FLAG_NONE,
+                stats: Stats | None = None) -> np.ndarray:
+    """rt_render_rgb8: render + toByte on the device(s), RGB bytes."""
+    out = np.zeros((height, width, 3), dtype=np.uint8)
+    st = stats if stats is not None else Stats()
+    rc = amd_lib().rt_render_rgb8(scene.handle, width, height, mode, flags, n_gpus,
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(st))
+    if rc != RT_OK:
+        raise RTError(rc, last_error())
+    return out
+
+
+def dist_rows(H: int, world: int, rank: int) -> list[int]:
+    """rt_dist_rows: the output rows rank renders (interleaved strips)."""
+    buf = (C.c_int32 * max(1, H))()
+    n = amd_lib().rt_dist_rows(H, world, rank, buf)
+    if n < 0:
+        raise RTError(n, "rt_dist_rows: bad arguments")
+    return list(buf[:n])
+
+
+def render_dist_sim(scene: Scene, width: int, height: int, mode: int, world: int, rgb8: bool = False,
+                    flags: int = RT_FLAG_NONE) -> np.ndarray:
+    """rt_test_render_dist_sim: the multi-GPU frame path with `world` ranks
+    simulated on the current device (RCCL gather replaced by copies)."""
+    lib = amd_lib()
+    if rgb8:
+        out = np.zeros((height, width, 3), dtype=np.uint8)
+        rc = lib.rt_test_render_dist_sim(scene.handle, width, height, mode, flags, world, 1, None,
+                                         out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    else:
+        out = np.zeros((height, width, 3), dtype=np.float64)
+        rc = lib.rt_test_render_dist_sim(scene.handle, width, height, mode, flags, world, 0, out.ctypes.data_as(_dp),
+                                         None)
+    if rc != RT_OK:
+        raise RTError(rc, last_error())
+    return out
 
 
 def oracle_render(scene: Scene, width: int, height: int, mode: int, row0: int = 0, row1: int | None = None,

@@ -1,0 +1,178 @@
+"""Multi-GPU frame path and device output path
+through the C-ABI.
+
+* rt_render_multi(n_gpus=1) and the one-process-per-GPU rt_render_dist with
+  world 1 are bit-identical to rt_render (the reference loop,
+  raytracer/src/tracer.cpp:247-305).
+* The whole multi-rank data path - partition, row chunks, gather stage
+  layout, placement on the root, device toByte - runs on one GPU with the
+  ranks simulated (rt_test_render_dist_sim; RCCL replaced by device copies)
+  and must reproduce rt_render bit for bit, for 2, 3 and 8 ranks, odd frame
+  heights and frames with fewer rows than ranks x strip.
+* rt_render_rgb8 / rt_framebuffer_to_rgb8_device equal the host toByte
+  (core.h:313-316) on the same framebuffer, including NaN, infinities,
+  negative values and values half-way between two 8-bit levels.
+
+Real multi-device RCCL runs need more than one GPU (the driver's 8-GPU bench);
+here rt_render_multi with more devices than visible must fail loudly.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import scenes
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RAY = os.path.join(REPO, "raytracing-project_amd", "bin", "ray")
+
+CASES = {
+    "cfg4_std": (lambda: scenes.config_json(4, dpi=40)[0], 0),
+    "cfg5_paper": (lambda: scenes.config_json(5, dpi=40)[0], 1),
+    "cfg2_std": (lambda: scenes.config_json(2, dpi=30)[0], 0),
+    "snorlax_paper": (lambda: json.dumps(scenes.with_dpi(scenes.load_example("snorlax"), 20)), 1),
+}
+
+
+def _scene(rt, name):
+    text, mode = CASES[name]
+    sc = rt.load_scene_from_json_text(text())
+    return sc, mode
+
+
+def _odd(text, w, h, dpi=16):
+    d = json.loads(text)
+    scr = d["screen"]
+    dims = scr.get("dimensions", [1, 1])
+    cx, cy = scr["position"][0] + dims[0] / 2, scr["position"][1] + dims[1] / 2
+    scr["dpi"] = dpi
+    scr["dimensions"] = [w / dpi, h / dpi]
+    scr["position"] = [cx - w / dpi / 2, cy - h / dpi / 2, scr["position"][2]]
+    return json.dumps(d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_render_multi_one_gpu_is_rt_render(gpu, name):
+    sc, mode = _scene(gpu, name)
+    W, H = sc.width, sc.height
+    a = gpu.Tracer(sc, W, H, mode).render()
+    st = gpu.Stats()
+    b = gpu.render_multi(sc, W, H, mode, 1, stats=st)
+    assert np.array_equal(a, b)
+    assert st.n_gpus == 1
+    c = gpu.render_multi(sc, W, H, mode, 0)   # 0 = every visible device
+    if gpu.device_count() == 1:
+        assert np.array_equal(a, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_render_rgb8_is_host_tobyte(gpu, name):
+    sc, mode = _scene(gpu, name)
+    W, H = sc.width, sc.height
+    fb = gpu.Tracer(sc, W, H, mode).render()
+    st = gpu.Stats()
+    got = gpu.render_rgb8(sc, W, H, mode, 1, stats=st)
+    assert np.array_equal(got, gpu.to_rgb8(fb))
+    assert st.ms_tobyte > 0.0 and st.ms_d2h > 0.0
+
+
+@pytest.mark.gpu
+def test_device_tobyte_special_values(gpu):
+    import torch
+
+    v = np.array([np.nan, -np.nan, np.inf, -np.inf, -1.0, -0.0, 0.0, 1e-300, 0.5 / 255, 1.5 / 255, 2.5 / 255,
+                  127.5 / 255, 254.5 / 255, 0.999999, 1.0, 1.0000001, 7.0, 0.5, np.nextafter(0.5 / 255, 1.0),
+                  np.nextafter(0.5 / 255, 0.0)], dtype=np.float64)
+    rng = np.random.default_rng(7)
+    halfway = (rng.integers(0, 255, 600) + 0.5) / 255.0
+    v = np.concatenate([v, halfway, rng.uniform(-0.2, 1.2, 3000)])
+    v = np.pad(v, (0, (-len(v)) % 3))
+    want = gpu.to_rgb8(v.reshape(-1, 1, 3)).reshape(-1)
+    d_in = torch.from_numpy(v).cuda()
+    d_out = torch.zeros(len(v), dtype=torch.uint8, device="cuda")
+    rc = gpu.amd_lib().rt_framebuffer_to_rgb8_device(C.c_void_p(d_in.data_ptr()), len(v) // 3,
+                                                     C.c_void_p(d_out.data_ptr()), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("name", ["cfg4_std", "cfg5_paper"])
+def test_dist_path_simulated_ranks(gpu, world, name):
+    sc, mode = _scene(gpu, name)
+    W, H = sc.width, sc.height
+    want = gpu.Tracer(sc, W, H, mode).render()
+    got = gpu.render_dist_sim(sc, W, H, mode, world)
+    assert np.array_equal(got, want)
+    got8 = gpu.render_dist_sim(sc, W, H, mode, world, rgb8=True)
+    assert np.array_equal(got8, gpu.to_rgb8(want))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,world", [(37, 29, 3), (24, 5, 8), (64, 61, 2)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dist_path_odd_frames(gpu, w, h, world, mode):
+    """Heights that leave partial strips and ranks without rows; paper mode
+    traces the neighbour rows of every strip (tracer.cpp:133-178)."""
+    sc = gpu.load_scene_from_json_text(_odd(scenes.config_json(4, dpi=24)[0], w, h))
+    assert (sc.width, sc.height) == (w, h)
+    want = gpu.Tracer(sc, w, h, mode).render()
+    assert np.array_equal(gpu.render_dist_sim(sc, w, h, mode, world), want)
+    assert np.array_equal(gpu.render_dist_sim(sc, w, h, mode, world, rgb8=True), gpu.to_rgb8(want))
+
+
+@pytest.mark.gpu
+def test_dist_world1_is_rt_render(gpu):
+    """One process per GPU with world 1: rt_dist_create / rt_render_dist."""
+    import torch
+
+    sc, mode = _scene(gpu, "cfg4_std")
+    W, H = sc.width, sc.height
+    lib = gpu.amd_lib()
+    uid = (C.c_uint8 * 128)()
+    assert lib.rt_dist_get_id(uid) == 0
+    d = C.c_void_p()
+    assert lib.rt_dist_create(uid, 1, 0, C.byref(d)) == 0, gpu.last_error()
+    try:
+        out = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+        st = gpu.Stats()
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, C.c_void_p(out.data_ptr()), None, C.byref(st))
+        assert rc == 0, gpu.last_error()
+        assert np.array_equal(out.cpu().numpy(), gpu.Tracer(sc, W, H, mode).render())
+        out8 = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+        rc = lib.rt_render_dist_rgb8(d, sc.handle, W, H, mode, 0, C.c_void_p(out8.data_ptr()), None, C.byref(st))
+        assert rc == 0, gpu.last_error()
+        assert np.array_equal(out8.cpu().numpy(), gpu.to_rgb8(out.cpu().numpy()))
+    finally:
+        lib.rt_dist_destroy(d)
+
+
+@pytest.mark.gpu
+def test_render_multi_more_gpus_than_visible_fails_loudly(gpu):
+    sc, mode = _scene(gpu, "cfg2_std")
+    n = gpu.device_count()
+    with pytest.raises(gpu.RTError) as e:
+        gpu.render_multi(sc, sc.width, sc.height, mode, n + 1)
+    assert e.value.code == gpu.RT_ERR_INVALID_ARG and "GPUs requested" in str(e.value)
+
+
+@pytest.mark.gpu
+def test_cli_stats_wall_clock_split(gpu, tmp_path):
+    scene = scenes.with_dpi(scenes.load_example("pokeballs"), 40)
+    js = tmp_path / "p.json"
+    js.write_text(json.dumps(scene))
+    out = tmp_path / "p.png"
+    r = subprocess.run([RAY, str(js), str(out), "--stats", "--gpus", "1", "--threads", "4"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("ms_load", "ms_rng", "ms_kernel", "ms_gather", "ms_tobyte", "ms_d2h", "ms_render", "ms_png", "ms_main"):
+        assert k in st and st[k] >= 0.0, k
+    assert st["n_gpus"] == 1 and st["ms_kernel"] > 0 and st["ms_main"] >= st["ms_render"]

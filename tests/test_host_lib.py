@@ -32,7 +32,28 @@ def test_libraries_export_every_declared_symbol():
     assert len(declared) >= 18 and "rt_render" in declared and "rt_last_error" in declared
     for name in declared:
         assert hasattr(host, name) or hasattr(amd, name), name
-    assert amd.rt_abi_version() == 2
+    assert amd.rt_abi_version() == 3
+
+
+@pytest.mark.parametrize("H,world", [(2160, 8), (2160, 3), (1080, 2), (17, 4), (5, 8), (1, 1)])
+def test_dist_partition(rt, H, world):
+    """rt_dist_rows: interleaved RT_STRIP_ROWS strips, every
+    output row on exactly one rank, ascending per rank, balanced to a strip."""
+    rows = [rt.dist_rows(H, world, r) for r in range(world)]
+    flat = sorted(x for rr in rows for x in rr)
+    assert flat == list(range(H))
+    for r, rr in enumerate(rows):
+        assert rr == sorted(rr)
+        assert all((x // 8) % world == r for x in rr)
+    sizes = [len(rr) for rr in rows]
+    assert max(sizes) - min(sizes) <= 8
+
+
+def test_dist_partition_matches_python_mirror(rt):
+    import frame_dist
+    for H, world in [(2160, 8), (1081, 3), (7, 2)]:
+        for r in range(world):
+            assert rt.dist_rows(H, world, r) == frame_dist.strip_rows(H, r, world)
 
 
 def _decode_png(path):
