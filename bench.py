@@ -4,23 +4,35 @@
 Metric: Mrays/s (primary + secondary) and wall-clock per frame on config 4:
 examples/snorlax.json at 3840x2160, 5 lights, recursion 4.
 A "ray" is one Scene::intersect or Scene::occluded query of the reference
-(raytracer/src/scene.cpp:10,33).  A "step" renders one whole frame: jitter
-stream generation (mt19937 jump-ahead) + trace kernels, with the scene and
-all buffers resident on the device; for N > 1 each rank renders interleaved
-8-row strips of the SAME frame (strong scaling) and rank 0 receives all rows
-with one RCCL all_gather over xGMI and scatters them into the frame.
+(raytracer/src/scene.cpp:10,33).  A "step" renders one whole frame through the
+product path rt_render_dist (include/rt.h): jitter stream (mt19937 jump-ahead)
++ trace kernels, with the scene resident on the device and the frame left in
+HBM on rank 0.  For N > 1 (one process per GPU, torch.distributed.run) every
+rank renders interleaved 8-row strips of the SAME frame (strong scaling) and
+rank 0 receives them through RCCL ncclGather over xGMI inside librtamd.
+
+After the timed region (never inside it): op-counted passes for the FLOP
+model, the wall-clock split of the CLI's end-to-end path (render + device
+toByte + D2H + parallel PNG, and the `ray` binary itself), kernel resources
+and occupancy, the trace kernel's HBM traffic from rocprofv3 PMC passes over
+the same frame, and the CPU baseline (the C port of the reference path,
+oracle/oracle.c, on a whole frame over the host cores plus a 1-thread band).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4]
-For N > 1 the driver launches one process per GPU with torch.distributed.run.
 """
 from __future__ import annotations
 
 import argparse
+import csv
 import ctypes as C
+import glob
 import json
 import os
 import platform
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -28,6 +40,8 @@ sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
 FP64_VALU_PEAK_TFLOPS = 78.6   # MI355X FP64 vector: 256 CU x 64 lanes x 2 x 2.4 GHz
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table
+JITTER_BYTES_PER_PX = 128      # 8 samples x (dx, dy) doubles, read once by the trace kernel
+FB_BYTES_PER_PX = 24           # RGB doubles written once
 
 
 def model_flops(ops: dict, primary: int, paper: bool) -> tuple[float, dict]:
@@ -48,19 +62,55 @@ def model_flops(ops: dict, primary: int, paper: bool) -> tuple[float, dict]:
     return float(f), {"pow": ops["shade_spec"], "acos": ops["poke_region"]}
 
 
+def pmc_traffic(config: int, timeout: int = 120) -> dict | None:
+    """HBM bytes per launch of the trace kernel, measured by rocprofv3 PMC
+    passes (one counter per pass, no tracing domains) over tools/one_frame.py
+    renders of the same frame.  FETCH_SIZE is doubled per the gfx950
+    calibration and both counters are KiB (MI355X_MICROARCH.md §HBM)."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="rt_pmc_")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, ctr)
+            cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", ctr, "--output-format", "csv", "-d", out,
+                   "-o", "pmc", "--", sys.executable, os.path.join(REPO, "tools", "one_frame.py"), "--config",
+                   str(config), "--frames", "2"]
+            r = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO)
+            if r.returncode != 0:
+                return {"error": f"{ctr} pass rc={r.returncode}"}
+            per = []
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                for row in csv.DictReader(open(f)):
+                    n = row.get("Kernel_Name", "")
+                    if ("k_std" in n or "k_paper_primary" in n) and row.get("Counter_Name") == ctr:
+                        per.append(float(row["Counter_Value"]))
+            if not per:
+                return {"error": f"{ctr}: no trace-kernel rows"}
+            vals[ctr] = sum(per) / len(per)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write = vals["WRITE_SIZE"] * 1024.0
+    return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=4)
-    ap.add_argument("--cpu-rows", type=int, default=64, help="rows in the CPU-oracle baseline sample")
+    ap.add_argument("--cpu-rows", type=int, default=64, help="rows of the 1-thread CPU-oracle band")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI wall-clock leg")
     ap.add_argument("--no-cull", action="store_true", help="disable wave-uniform bound culling")
     ap.add_argument("--fp32", action="store_true",
                     help="time the NON-PARITY FP32 fast path as the headline (RT_FLAG_FP32); default is FP64")
-    ap.add_argument("--fp32-steps", type=int, default=3, help="frames of the FP32 side leg (0 = skip)")
-    ap.add_argument("--chunks", type=int, default=4, help="row chunks per rank pipelined with the gather (N > 1)")
+    ap.add_argument("--fp32-steps", type=int, default=20, help="frames of the FP32 side leg (0 = skip)")
     args = ap.parse_args()
 
     import numpy as np
@@ -70,16 +120,15 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
 
-    import frame_dist
     import rtamd
     import scenes
-    from frame_dist import STRIP
 
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
@@ -88,83 +137,82 @@ def main() -> int:
     flags = rtamd.RT_FLAG_NO_CULL if args.no_cull else rtamd.RT_FLAG_NONE
     if args.fp32:
         flags |= rtamd.RT_FLAG_FP32
-    dev = torch.device("cuda", local)
 
-    df = frame_dist.DistFrame(W, H, rank, world, dev, chunks=args.chunks)
-    rows = df.rows
-    n_rows = len(rows)
-    rows_c = (C.c_int32 * max(1, n_rows))(*rows)
+    # the product's distribution: rank 0 makes the RCCL id, every rank binds its GPU
+    uid = (C.c_uint8 * 128)()
+    if rank == 0 and lib.rt_dist_get_id(uid) != 0:
+        raise RuntimeError(rtamd.last_error())
+    if dist:
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
+        dist.broadcast(t, src=0)
+        uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+    dh = C.c_void_p()
+    if lib.rt_dist_create(uid, world, rank, C.byref(dh)) != 0:
+        raise RuntimeError(f"rt_dist_create failed: {rtamd.last_error()}")
+    n_rows = len(rtamd.dist_rows(H, world, rank))
+    frame = torch.zeros((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
+    frame_ptr = C.c_void_p(frame.data_ptr()) if frame is not None else None
     stream = torch.cuda.current_stream(dev)
-    # chunks alternate between two streams so one chunk's launch tail overlaps the next chunk
-    streams = [stream, torch.cuda.Stream(dev)]
     st = rtamd.Stats()
 
-    def scatter(src, slot_rows, full):
-        rc = lib.rt_scatter_rows_device(C.c_void_p(src.data_ptr()), C.c_void_p(slot_rows.data_ptr()),
-                                        slot_rows.numel(), W, C.c_void_p(full.data_ptr()),
-                                        C.c_void_p(stream.cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"rt_scatter_rows_device failed ({rc}): {rtamd.last_error()}")
-
     def step(f=flags, stats=st):
-        # one frame: jitter stream of this rank's rows (rt_frame_begin), the
-        # trace chunk by chunk, each chunk gathered to rank 0 over RCCL while
-        # the next one is traced (frame_dist.DistFrame), scatter on rank 0
-        fr = C.c_void_p()
-        rc = lib.rt_frame_begin(sc.handle, W, H, mode, f, rows_c, n_rows, C.c_void_p(stream.cuda_stream),
-                                C.byref(fr))
+        rc = lib.rt_render_dist(dh, sc.handle, W, H, mode, f, frame_ptr, C.c_void_p(stream.cuda_stream),
+                                C.byref(stats))
         if rc != 0:
-            raise RuntimeError(f"rt_frame_begin failed ({rc}): {rtamd.last_error()}")
-        err = []
+            raise RuntimeError(f"rt_render_dist failed ({rc}): {rtamd.last_error()}")
 
-        def trace_chunk(a, b, out, s):
-            r = lib.rt_frame_trace(fr, a, b, C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream))
-            if r != 0:
-                err.append((r, rtamd.last_error()))
-
-        try:
-            df.run(trace_chunk, dist, scatter, streams)
-        finally:
-            rc = lib.rt_frame_end(fr, C.byref(stats))
-        if err or rc != 0:
-            raise RuntimeError(f"frame failed: {err or rc} {rtamd.last_error()}")
-
-    for _ in range(args.warmup):
+    t_first = time.perf_counter()
+    step()   # first frame: kernels load, jitter plan + checkpoint table, scene upload
+    first_ms = (time.perf_counter() - t_first) * 1e3
+    for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, rng_ms, rays_local = [], [], 0
+    kernel_ms, rng_ms, gather_ms, rays_local, traced_local = [], [], [], 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         kernel_ms.append(st.ms_kernel)
         rng_ms.append(st.ms_rng)
+        gather_ms.append(st.ms_gather)
         rays_local += st.rays_intersect + st.rays_occluded
+        traced_local += st.rays_traced
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    k_ms = sum(kernel_ms) / len(kernel_ms)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, k_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([rays_local], dtype=torch.float64, device=dev)
+        elapsed, k_ms_max = float(t[0].item()), float(t[1].item())
+        r = torch.tensor([rays_local, traced_local], dtype=torch.float64, device=dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        rays_total = float(r.item())
+        rays_total, traced_total = float(r[0].item()), float(r[1].item())
     else:
-        rays_total = float(rays_local)
+        k_ms_max, rays_total, traced_total = k_ms, float(rays_local), float(traced_local)
 
     # Instrumented passes (outside the timed region) for the FLOP model:
     # culling off = the reference's own primitive calls one for one
     # (tests/test_gpu_parity.py::test_opcounts_match_reference_without_cull),
     # culling on = what this kernel actually executed.
-    st_ops = rtamd.Stats()
-    step(flags | rtamd.RT_FLAG_COUNT_OPS | rtamd.RT_FLAG_NO_CULL, st_ops)
-    st_exe = rtamd.Stats()
-    step(flags | rtamd.RT_FLAG_COUNT_OPS, st_exe)
+    def counted_pass(f):
+        s = rtamd.Stats()
+        step(f, s)
+        v = [int(s.ops[i]) for i in range(16)] + [int(s.rays_occluded)]
+        if dist:
+            tv = torch.tensor(v, dtype=torch.float64, device=dev)
+            dist.all_reduce(tv, op=dist.ReduceOp.SUM)
+            v = [int(x) for x in tv.cpu().tolist()]
+        d = {rtamd.OP_NAMES[i]: v[i] for i in range(16)}
+        d["_occluded"] = v[16]
+        return d
+
+    ops_ref = counted_pass(flags | rtamd.RT_FLAG_COUNT_OPS | rtamd.RT_FLAG_NO_CULL)
+    ops_exe = counted_pass(flags | rtamd.RT_FLAG_COUNT_OPS)
     torch.cuda.synchronize()
 
     # Side leg (outside the timed region, not the headline): the NON-PARITY
@@ -188,7 +236,7 @@ def main() -> int:
             dist.barrier()
         e32 = time.perf_counter() - t32
         if dist:
-            t = torch.tensor([e32, rays32], dtype=torch.float64, device=dev)
+            t = torch.tensor([e32], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             e32 = float(t[0].item())
             r = torch.tensor([rays32], dtype=torch.float64, device=dev)
@@ -202,59 +250,105 @@ def main() -> int:
     if rank != 0:
         if dist:
             dist.barrier()
+        lib.rt_dist_destroy(dh)
+        if dist:
             dist.destroy_process_group()
         return 0
 
-    def counted(s):
-        d = {rtamd.OP_NAMES[i]: int(s.ops[i]) for i in range(16)}
-        d["_occluded"] = int(s.rays_occluded)
-        return d
-
-    primary = n_rows * W * (1 if mode == 1 else 8)
-    flops, transc = model_flops(counted(st_ops), primary, mode == 1)
-    flops_exe, _ = model_flops(counted(st_exe), primary, mode == 1)
-    k_ms = sum(kernel_ms) / len(kernel_ms)
-    achieved = flops / (k_ms * 1e-3) / 1e12
+    primary = H * W * (1 if mode == 1 else 8)
+    flops, transc = model_flops(ops_ref, primary, mode == 1)
+    flops_exe, _ = model_flops(ops_exe, primary, mode == 1)
+    achieved = flops / (k_ms_max * 1e-3) / 1e12 / world   # per GPU: each rank's kernel covers 1/world of the frame
     value = rays_total / elapsed / 1e6
     rays_per_frame = rays_total / args.steps
 
-    prof_traffic = None
-    tpath = os.path.join(REPO, "profiles", "traffic.json")
-    if os.path.exists(tpath):
+    # Wall-clock split of the CLI's end-to-end path, N = 1:
+    # render + device toByte + D2H of 3 B/px (rt_render_rgb8), the parallel
+    # PNG deflate, and the `ray` binary itself (process start to exit).
+    wall = {"rng": round(sum(rng_ms) / len(rng_ms), 3), "kernel": round(k_ms, 3),
+            "gather": round(sum(gather_ms) / len(gather_ms), 3)}
+    if world == 1:
+        s8 = rtamd.Stats()
+        rtamd.render_rgb8(sc, W, H, mode, 1, flags, s8)
+        tr = time.perf_counter()
+        rgb = rtamd.render_rgb8(sc, W, H, mode, 1, flags, s8)
+        wall["render_rgb8_total"] = round((time.perf_counter() - tr) * 1e3, 3)
+        wall["tobyte"] = round(s8.ms_tobyte, 3)
+        wall["d2h"] = round(s8.ms_d2h, 3)
+        nt = max(1, min(16, os.cpu_count() or 1))
+        with tempfile.TemporaryDirectory() as td:
+            tp = time.perf_counter()
+            rtamd.write_png(os.path.join(td, "f.png"), rgb, threads=nt)
+            wall["png"] = round((time.perf_counter() - tp) * 1e3, 3)
+            wall["png_threads"] = nt
+            if not args.no_cli:
+                js = os.path.join(td, "scene.json")
+                with open(js, "w") as f:
+                    f.write(text)
+                cmd = [os.path.join(REPO, "raytracing-project_amd", "bin", "ray"), js, os.path.join(td, "cli.png")]
+                cmd += (["--paper"] if mode == 1 else []) + ["--stats", "--threads", str(nt)]
+                tc = time.perf_counter()
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+                wall["cli_total"] = round((time.perf_counter() - tc) * 1e3, 3)
+                if r.returncode == 0:
+                    cs = json.loads(r.stdout.strip().splitlines()[-1])
+                    wall["cli_split"] = {k: cs[k] for k in ("ms_load", "ms_rng", "ms_kernel", "ms_tobyte", "ms_d2h",
+                                                            "ms_render", "ms_png", "ms_main")}
+                else:
+                    wall["cli_error"] = r.stderr[-300:]
+        wall["note"] = ("cli_total = the `ray` process end to end (HIP init, JSON load, first-frame device "
+                        "setup, render, PNG); cli_split = its own timers")
+
+    # Kernel resources / occupancy of the timed trace kernel.
+    ki = (C.c_int32 * 8)()
+    occupancy = None
+    if lib.rt_test_kernel_info(sc.handle, mode, flags, ki) == 0:
+        occupancy = {"vgprs": ki[0], "scratch_bytes_per_lane": ki[1], "lds_bytes": ki[2],
+                     "workgroups_per_cu": ki[3], "waves_per_simd": ki[4], "max_waves_per_simd": 8}
+
+    # HBM: algorithmic bytes of the trace kernel per launch vs counter-measured traffic.
+    px = n_rows * W
+    alg_bytes = px * (FB_BYTES_PER_PX + (JITTER_BYTES_PER_PX if mode == 0 else 0))
+    traffic = None
+    if world == 1 and not args.no_pmc:
         try:
-            with open(tpath) as f:
-                tj = json.load(f)
-            if tj.get("config") == args.config and world == 1:
-                prof_traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            prof_traffic = None
+            traffic = pmc_traffic(args.config)
+        except Exception as e:   # profiler unavailable: report, do not fail the bench
+            traffic = {"error": str(e)[:200]}
 
     cpu = None
     if not args.no_cpu and world == 1:
-        # bounded sample: a band of rows from the middle of the same frame,
-        # single-threaded CPU oracle (C port of the reference path)
+        nt = max(1, min(16, os.cpu_count() or 1))
+        tc = time.perf_counter()
+        _, ostm = rtamd.oracle_render(sc, W, H, mode, 0, H, threads=nt)
+        dtm = time.perf_counter() - tc
+        raysm = ostm.rays_intersect + ostm.rays_occluded
+        cpu = {"value": round(raysm / dtm / 1e6, 4), "unit": "Mrays/s", "cores": nt, "kind": "port",
+               "sample": f"whole config-{args.config} frame {W}x{H}: {raysm} rays in {dtm:.1f} s on {nt} threads "
+                         f"(oracle/oracle.c, rows split across threads; {platform.machine()} host)"}
+        # faithful to the reference: one thread, a band through the middle of the frame
         r0 = max(0, H // 2 - args.cpu_rows // 2)
         r1 = min(H, r0 + args.cpu_rows)
         tc = time.perf_counter()
         _, ost = rtamd.oracle_render(sc, W, H, mode, r0, r1, threads=1)
         dt = time.perf_counter() - tc
         cpu_rays = ost.rays_intersect + ost.rays_occluded
-        cpu = {"value": round(cpu_rays / dt / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "port",
-               "sample": f"config {args.config} output rows [{r0},{r1}) x {W} px, {cpu_rays} rays in {dt:.1f} s "
-                         f"on {platform.processor() or platform.machine()} (oracle/oracle.c, 1 thread)"}
-        # the same port over all the cores this job may use
-        # (rows split across pthreads; the box grants 16), a 4x larger band
-        nt = max(1, min(16, os.cpu_count() or 1))
-        r0m = max(0, H // 2 - 2 * args.cpu_rows)
-        r1m = min(H, r0m + 4 * args.cpu_rows)
-        tc = time.perf_counter()
-        _, ostm = rtamd.oracle_render(sc, W, H, mode, r0m, r1m, threads=nt)
-        dtm = time.perf_counter() - tc
-        raysm = ostm.rays_intersect + ostm.rays_occluded
-        cpu["all_cores"] = {"value": round(raysm / dtm / 1e6, 4), "cores": nt,
-                            "sample": f"output rows [{r0m},{r1m}) x {W} px, {raysm} rays in {dtm:.1f} s"}
+        cpu["one_thread"] = {"value": round(cpu_rays / dt / 1e6, 4), "cores": 1,
+                             "sample": f"output rows [{r0},{r1}) x {W} px, {cpu_rays} rays in {dt:.1f} s"}
 
     name = scenes.CONFIGS[args.config][0]
+    hbm = {"algorithmic_bytes_per_launch": alg_bytes,
+           "algorithmic_GBs": round(alg_bytes / (k_ms * 1e-3) / 1e9, 1),
+           "algorithmic_frac": round(alg_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    traffic_bytes = None
+    if traffic and "bytes" in traffic:
+        traffic_bytes = traffic["bytes"]
+        hbm.update({"counter_fetch_bytes": traffic["fetch_bytes"], "counter_write_bytes": traffic["write_bytes"],
+                    "counter_frac": round(traffic_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                    "counter_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/one_frame.py in "
+                                      "this run (FETCH x2, KiB -> B: MI355X_MICROARCH.md §HBM)"})
+    elif traffic:
+        hbm["counter_error"] = traffic.get("error")
     out = {
         "metric": "Mrays/s (primary+secondary) + wall-clock per frame, 4K scene @1/2/4/8 GPU",
         "value": round(value, 3),
@@ -269,23 +363,26 @@ def main() -> int:
         "dtype": "f32" if args.fp32 else "f64",
         "data": "synthetic: reference example scene JSON + mt19937(12345) jitter, rendered on device",
         "config": {"workload": name, "width": W, "height": H, "mode": "paper" if mode else "standard",
-                   "rays_per_frame": int(rays_per_frame), "parallelism": f"row-strips{STRIP}x{world}" + (f", gather-to-rank0 in {len(df.bounds)} chunks" if world > 1 else ""),
+                   "rays_per_frame": int(rays_per_frame), "rays_traced_per_frame": int(traced_total / args.steps),
+                   "parallelism": f"row-strips8x{world}" + (", RCCL ncclGather to rank 0 in 4 chunks" if world > 1
+                                                            else ""),
                    "cull": not args.no_cull},
         "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
-                     "traffic": prof_traffic, "kernel": "k_std" if mode == 0 else "k_paper_primary",
-                     "kernel_ms": round(k_ms, 3), "flops_per_launch": flops, "transcendentals": transc,
+                     "traffic": traffic_bytes, "kernel": "k_std" if mode == 0 else "k_paper_primary",
+                     "kernel_ms": round(k_ms, 3), "flops_per_launch": flops / world, "transcendentals": transc,
                      "flops_model": "SURVEY.md 8d table x the reference's own primitive calls (GPU counters, "
                                     "culling off; equal to the CPU oracle's by test)",
-                     "executed_flops_per_launch": flops_exe,
-                     "executed_frac": round(flops_exe / (k_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
-                     "hbm_frac": None if prof_traffic is None else
-                     round(prof_traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)},
-        "rng_ms": round(sum(rng_ms) / len(rng_ms), 3),
+                     "executed_flops_per_launch": flops_exe / world,
+                     "executed_frac": round(flops_exe / world / (k_ms_max * 1e-3) / 1e12 / FP64_VALU_PEAK_TFLOPS, 4),
+                     "occupancy": occupancy, "hbm": hbm},
+        "wall_clock_ms": wall,
+        "first_frame_ms": round(first_ms, 1),
         "cpu_baseline": cpu,
         "fp32_fast_path": fp32,
     }
     print(json.dumps(out), flush=True)
+    lib.rt_dist_destroy(dh)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

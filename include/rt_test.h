@@ -21,7 +21,9 @@ int rt_test_mt_jump_cpu(int K_blocks, int levels);
 /* GPU: generate the jitter stream for output indices [q0, q1) (even) with the
  * device jump/fill kernels at segment length K_blocks twist blocks and copy
  * uniform draws [first, first+count) (draw index = output index / 2) to
- * out_host.  Returns an rt_status. */
+ * out_host.  K_blocks == 0 selects the frame path instead: the resident
+ * checkpoint table (every 64 twist blocks, built by the same jump tree) and
+ * the one-wavefront fill kernel.  Returns an rt_status. */
 int rt_test_jitter_device(int K_blocks, int64_t q0, int64_t q1, int64_t first, int64_t count, double* out_host);
 
 /* Host-only: compile a scene to its device object table and report
@@ -30,6 +32,13 @@ int rt_test_jitter_device(int K_blocks, int64_t q0, int64_t q1, int64_t first, i
  * programs, max CSG operand depth}.  No device is touched. */
 struct rt_scene;
 int rt_test_compile_info(const struct rt_scene* s, int32_t* out);
+
+/* Resources of the trace kernel rt_render would launch for this scene, mode
+ * and flags (hipFuncGetAttributes + occupancy query): out[8] = {VGPRs per
+ * lane, scratch bytes per lane, static LDS bytes per workgroup, resident
+ * workgroups per CU, waves per SIMD, max threads per block, wave-level
+ * culling variant, reflection/refraction variant}.  Needs a device. */
+int rt_test_kernel_info(const struct rt_scene* s, int mode, int flags, int32_t* out);
 
 /* GPU, one device: the multi-GPU frame path of rt_render_multi /
  * rt_render_dist (partition, row chunks, gather stage layout, placement on

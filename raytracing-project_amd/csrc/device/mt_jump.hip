@@ -255,9 +255,221 @@ inline int64_t ckpt_parent(int64_t c) {
     return c - (c / lo) * lo;
 }
 
+// Consolidate the partial windows of checkpoints [c0, c1) into the table.
+__global__ void k_mt_consolidate(const uint32_t* __restrict__ ckpt, JumpArgs A, int64_t c0, int64_t c1,
+                                 uint32_t* __restrict__ table) {
+    const int64_t c = c0 + blockIdx.x;
+    if (c >= c1) return;
+    const int np = ckpt_parts(c, A.parts);
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        uint32_t v = 0;
+        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)c * rtamd::kMTParts + p) * N + k];
+        table[(size_t)c * N + k] = v;
+    }
+}
+
+// Workgroup = ONE wavefront per segment of kTableK blocks.  The segment's
+// window comes from the checkpoint table; per block the wave converts the
+// current block into draws (312 output pairs, ~5 per lane) and twists the
+// next block into the other half of a 2-block LDS ring (227 lanes' worth of
+// the three-word recurrence, ~4 per lane).  A single wave needs no
+// workgroup barrier, only LDS ordering, so blocks follow each other at the
+// wave's instruction rate and many segments share a SIMD.
+constexpr int FILLW_THREADS = 64;
+__global__ __launch_bounds__(FILLW_THREADS) void k_mt_fill_w(const uint32_t* __restrict__ table, FillArgs A,
+                                                             double* __restrict__ jit) {
+    __shared__ uint32_t buf[2 * N];
+    const int lane = threadIdx.x;
+    const int64_t c = A.segs[2 * blockIdx.x];
+    int r = (int)A.segs[2 * blockIdx.x + 1];
+    const int64_t seg_q = c * (int64_t)A.K * N;
+    const int64_t q_last = A.R[A.nr - 1].qb;
+    rtamd::JRange g0 = A.R[r];
+    rtamd::JRange g1 = r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
+    for (int k = lane; k < N; k += FILLW_THREADS) buf[k] = table[(size_t)c * N + k];
+    lds_barrier();
+    int base = 0;
+    for (int b = 0; b < A.K; ++b) {
+        const int64_t bq = seg_q + (int64_t)b * N;
+        if (bq >= q_last) break;
+        while (g0.qb <= bq) {   // uniform
+            if (++r >= A.nr) break;
+            g0 = g1;
+            g1 = r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
+        }
+        if (r >= A.nr) break;
+        const uint32_t* o = buf + base;
+        if (g0.qa < bq + N) {
+            const BlockDst d = block_dst(jit, bq, g0, g1, r, A.nr);
+            for (int i = lane; i < N / 2; i += FILLW_THREADS) {
+                double* dst = nullptr;
+                if (d.generic) {
+                    const int64_t q = generic_dst(bq + 2 * i, A, r);
+                    if (q >= 0) dst = jit + q;
+                } else if (i >= d.a0 && i < d.b0) {
+                    dst = d.p0 + i;
+                } else if (i >= d.a1 && i < d.b1) {
+                    dst = d.p1 + i;
+                }
+                if (dst) *dst = jitter_from(o[2 * i], o[2 * i + 1]);
+            }
+        }
+        if (b + 1 < A.K && bq + N < q_last) {
+            uint32_t* nw = buf + (base ^ N);
+            for (int t = lane; t < 227; t += FILLW_THREADS) {
+                const uint32_t n0 = twist_word(o[t], o[t + 1], o[t + 397]);
+                const uint32_t n1 = twist_word(o[227 + t], o[228 + t], n0);
+                nw[t] = n0;
+                nw[227 + t] = n1;
+                if (t < 170) {
+                    const uint32_t nx = (t == 169) ? twist_word(o[0], o[1], o[397]) : o[455 + t];
+                    nw[454 + t] = twist_word(o[454 + t], nx, n1);
+                }
+            }
+        }
+        lds_barrier();
+        base ^= N;
+    }
+}
+
+// Needed segments of a job (with the first range overlapping each), in the
+// layout FillArgs::segs expects.
+std::vector<int64_t> job_segments(const std::vector<rtamd::JRange>& ranges, int64_t seg) {
+    std::vector<int64_t> segs;
+    size_t r = 0;
+    int64_t last = -1;
+    for (const rtamd::JRange& g : ranges) {
+        for (int64_t c = std::max(last + 1, g.qa / seg); c <= (g.qb - 1) / seg; ++c) {
+            while (r < ranges.size() && ranges[r].qb <= c * seg) ++r;
+            segs.push_back(c);
+            segs.push_back((int64_t)r);
+            last = c;
+        }
+    }
+    return segs;
+}
+
 }  // namespace
 
 namespace rtamd {
+
+hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
+    if (n_need <= n_ck) return hipSuccess;
+    const int64_t n_new = std::max<int64_t>(n_need, n_ck + n_ck / 4);
+    const int64_t q1 = n_new * (int64_t)kTableK * N;
+    const int levels = mt_levels_needed(kTableK, q1);
+    if (levels > MAX_LEVELS) return hipErrorInvalidValue;
+    hipError_t e = hipSuccess;
+    if (plan.K != kTableK || plan.levels < levels) {
+        e = plan.build(kTableK, levels);
+        if (e != hipSuccess) return e;
+    }
+    // every checkpoint of [0, n_new) by the radix-64 jump tree into partial
+    // windows, then consolidated into a new table
+    std::vector<int64_t> lists;
+    int64_t lvl_off[MAX_LEVELS + 1] = {0};
+    for (int j = 0; j < plan.levels; ++j) {
+        const int64_t lo = (int64_t)1 << (kMTRadixBits * j);
+        for (int64_t c = lo; c < std::min(n_new, lo * kMTRadix); ++c) lists.push_back(c);
+        lvl_off[j + 1] = (int64_t)lists.size();
+    }
+    uint32_t* d_ckpt = nullptr;
+    int64_t* d_list = nullptr;
+    uint32_t* d_tab = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    e = hipMalloc(&d_ckpt, (size_t)n_new * kMTParts * N * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&d_list, std::max<size_t>(1, lists.size()) * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMalloc(&d_tab, (size_t)n_new * N * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess && !lists.empty())
+        e = hipMemcpyAsync(d_list, lists.data(), lists.size() * sizeof(int64_t), hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess) e = hipEventRecord(e0, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_ckpt, plan.d_base, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
+    int8_t parts[MAX_LEVELS] = {1, 1, 1, 1, 1, 1, 1, 1};
+    for (int j = 0; j < plan.levels; ++j) {
+        const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
+        if (n_j > 0) parts[j] = (int8_t)level_parts(n_j);
+    }
+    JumpArgs A{};
+    for (int k = 0; k < MAX_LEVELS; ++k) A.parts[k] = parts[k];
+    for (int j = 0; j < plan.levels && e == hipSuccess; ++j) {
+        const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
+        if (n_j <= 0) continue;
+        A.lo = (int64_t)1 << (kMTRadixBits * j);
+        A.list = d_list + lvl_off[j];
+        A.S = parts[j];
+        for (int m = 0; m < kMTRadix; ++m) {
+            A.off[m] = plan.off[(size_t)j * kMTRadix + m];
+            A.len[m] = plan.off[(size_t)j * kMTRadix + m + 1] - A.off[m];
+        }
+        hipLaunchKernelGGL(k_mt_jump, dim3((unsigned)n_j, (unsigned)A.S), dim3(JUMP_THREADS), 0, stream, plan.d_taps,
+                           A, d_ckpt);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_mt_consolidate, dim3((unsigned)n_new), dim3(256), 0, stream, d_ckpt, A, (int64_t)0,
+                           n_new, d_tab);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) (void)hipEventElapsedTime(&ms_last_build, e0, e1);
+    if (d_ckpt) (void)hipFree(d_ckpt);
+    if (d_list) (void)hipFree(d_list);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e != hipSuccess) {
+        if (d_tab) (void)hipFree(d_tab);
+        return e;
+    }
+    if (d_table) (void)hipFree(d_table);
+    d_table = d_tab;
+    n_ck = cap = n_new;
+    return hipSuccess;
+}
+
+void JitterTable::release() {
+    if (d_table) (void)hipFree(d_table);
+    d_table = nullptr;
+    n_ck = cap = 0;
+    plan.release();
+}
+
+size_t mt_fill_scratch_bytes(const std::vector<JRange>& ranges) {
+    if (ranges.empty()) return 64;
+    const int64_t n_ck = (ranges.back().qb - 1) / ((int64_t)kTableK * N) + 1;
+    return ranges.size() * sizeof(JRange) + (size_t)n_ck * 2 * sizeof(int64_t) + 64;
+}
+
+hipError_t mt_launch_fill(const JitterTable& T, const std::vector<JRange>& ranges, JitterJob& job, void* d_scratch,
+                          double* d_jit, hipStream_t stream) {
+    if (ranges.empty()) return hipSuccess;
+    for (size_t i = 0; i < ranges.size(); ++i) {
+        const JRange& g = ranges[i];
+        if (g.qa < 0 || g.qb <= g.qa || (g.qa & 1) || (g.qb & 1) || g.dst < 0 || (i && g.qa < ranges[i - 1].qb))
+            return hipErrorInvalidValue;
+    }
+    const int64_t seg = (int64_t)kTableK * N;
+    if ((ranges.back().qb - 1) / seg >= T.n_ck) return hipErrorInvalidValue;   // table too short
+    const std::vector<int64_t> segs = job_segments(ranges, seg);
+    const size_t b_r = ranges.size() * sizeof(JRange), b_s = segs.size() * sizeof(int64_t);
+    job.stage.resize(b_r + b_s);
+    std::memcpy(job.stage.data(), ranges.data(), b_r);
+    std::memcpy(job.stage.data() + b_r, segs.data(), b_s);
+    job.qmax = ranges.back().qb;
+    char* dsc = static_cast<char*>(d_scratch);
+    hipError_t e = hipMemcpyAsync(dsc, job.stage.data(), job.stage.size(), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    FillArgs F{};
+    F.K = kTableK;
+    F.nr = (int)ranges.size();
+    F.R = reinterpret_cast<const JRange*>(dsc);
+    F.segs = reinterpret_cast<const int64_t*>(dsc + b_r);
+    hipLaunchKernelGGL(k_mt_fill_w, dim3((unsigned)(segs.size() / 2)), dim3(FILLW_THREADS), 0, stream, T.d_table, F,
+                       d_jit);
+    return hipGetLastError();
+}
 
 hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
     release();

@@ -78,4 +78,26 @@ size_t mt_scratch_bytes(int K, const std::vector<JRange>& ranges);
 size_t mt_ckpt_words(int K, int64_t q1);
 int mt_levels_needed(int K, int64_t q1);
 
+// Checkpoint table: the generator's window at every kTableK-th twist block
+// from the start of the stream, i.e. constants of std::mt19937(12345) in the
+// same sense as the jump polynomials.  Computed once per device with the
+// GF(2) jump tree (k_mt_jump, on first use and again only when a frame needs
+// checkpoints beyond the table) and kept resident; every frame then
+// regenerates ALL of its jitter draws from it (k_mt_fill_w: one wavefront
+// per kTableK-block segment, no per-frame jumps).
+constexpr int kTableK = 64;
+struct JitterTable {
+    JitterPlan plan;                  // K = kTableK
+    uint32_t* d_table = nullptr;      // [cap][624] windows
+    int64_t n_ck = 0, cap = 0;        // checkpoints present / allocated
+    float ms_last_build = 0.f;        // device time of the last extension (diagnostics)
+    hipError_t ensure(int64_t n_need, hipStream_t stream);   // synchronous when it grows
+    void release();
+};
+// Scratch for mt_launch_fill's segment/range lists.
+size_t mt_fill_scratch_bytes(const std::vector<JRange>& ranges);
+// Regenerate the draws of `ranges` from the table (table.ensure must cover them).
+hipError_t mt_launch_fill(const JitterTable& T, const std::vector<JRange>& ranges, JitterJob& job, void* d_scratch,
+                          double* d_jit, hipStream_t stream);
+
 }  // namespace rtamd

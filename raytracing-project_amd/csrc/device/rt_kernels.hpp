@@ -347,6 +347,20 @@ void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const Scene
     }
 }
 
+// The kernel launch_std / launch_paper pick for a variant (resource queries).
+const void* std_kernel(bool e, bool d, bool sec, bool wv) {
+    if (e) return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
+    if (d) return sec ? (const void*)k_std<false, true, true, false> : (const void*)k_std<false, true, false, false>;
+    if (sec) return wv ? (const void*)k_std<false, false, true, false, true> : (const void*)k_std<false, false, true, false>;
+    return wv ? (const void*)k_std_lean<false, true> : (const void*)k_std_lean<false, false>;
+}
+
+const void* paper_kernel(bool e, bool d, bool wv) {
+    if (e) return (const void*)k_paper_primary<true, true, false>;
+    if (d) return (const void*)k_paper_primary<false, true, false>;
+    return wv ? (const void*)k_paper_primary_lean<false, true> : (const void*)k_paper_primary_lean<false, false>;
+}
+
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {
     hipLaunchKernelGGL(k_paper_finish, grid, dim3(256), 0, st, P);
 }

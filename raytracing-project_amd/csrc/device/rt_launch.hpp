@@ -128,6 +128,8 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
     void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,               \
                       const rtamd::PaperParams& P);                                                               \
     void launch_paper_finish(dim3 grid, hipStream_t st, const rtamd::PaperParams& P);                             \
+    const void* std_kernel(bool e, bool d, bool sec, bool wv);                                                    \
+    const void* paper_kernel(bool e, bool d, bool wv);                                                            \
     }
 RT_DECLARE_LAUNCHERS(rtd)
 RT_DECLARE_LAUNCHERS(rtf)

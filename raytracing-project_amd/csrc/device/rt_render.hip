@@ -40,28 +40,6 @@ using rtamd::StdParams;
 
 namespace {
 
-constexpr int kJitterKMax = 1024;       // twist blocks per jitter segment, upper bound
-constexpr int kJitterKMin = 64;
-
-// Segment length for a jitter job.  A segment is regenerated serially by one
-// workgroup (latency ~ K twist blocks, ~0.6 us each); a checkpoint costs one
-// GF(2) jump (a ~10k-tap correlation over 20k words in LDS).  Aim at a few
-// hundred segments for the words the job needs: enough workgroups to fill
-// the chip, few enough that the jumps stay cheap (measured with
-// tools/sim_ranks.py on config 4: 1024 for a 4K frame, 256-512 for a
-// 1/8-frame rank; small frames get short segments).  RT_JITTER_K overrides
-// (diagnostics).
-int jitter_k(int64_t words_needed) {
-    static const int env_k = [] {
-        const char* e = std::getenv("RT_JITTER_K");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (env_k > 0) return env_k;
-    int K = kJitterKMax;
-    while (K > kJitterKMin && words_needed / (624 * 128) < K) K >>= 1;
-    return K;
-}
-
 __global__ void k_scatter_rows(const double* __restrict__ src, const int32_t* __restrict__ rows, int n_rows, int W,
                                double* __restrict__ dst) {
     const size_t row_len = (size_t)W * 3;
@@ -138,7 +116,7 @@ struct Workspace {
     DBuf nodes_f, mats_f, lights_f, dlights_f, fold_f;   // float copies (RT_FLAG_FP32)
     DBuf rows, jit, ckpt, jscratch, counters;
     DBuf paper_i, paper_d, paper_aux, fb;
-    std::map<int, rtamd::JitterPlan> jplan;   // per segment length K
+    rtamd::JitterTable jtab;                  // mt19937(12345) checkpoint table (resident)
     rtamd::JitterJob jjob;
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -371,6 +349,14 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.Ly = d.camera.Ly;
     S.medium_index = d.medium_index;
 
+    if (n_rows > 0 && mode == RT_MODE_STANDARD) {
+        // the checkpoint table must reach the last loop row's stream words
+        // (built on the first frame, extended only for a larger frame)
+        int max_y = 0;
+        for (int i = 0; i < n_rows; ++i) max_y = std::max(max_y, H - 1 - rows_host[i]);
+        const int64_t q_end = (int64_t)32 * W * (max_y + 1);
+        HIP_TRY(ws.jtab.ensure((q_end - 1) / ((int64_t)rtamd::kTableK * 624) + 1, st));
+    }
     HIP_TRY(hipEventRecord(ws.ev[0], st));
     if (n_rows > 0 && mode == RT_MODE_STANDARD) {
         // Loop row y = H-1-rows[ri] consumes outputs [32Wy, 32W(y+1))
@@ -394,23 +380,11 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
                 ws.jranges.push_back(rtamd::JRange{row_q * y, row_q * (y + 1), (int64_t)k * 16 * W});
         }
         const int64_t q1 = ws.jranges.back().qb;
-        const int K = jitter_k(row_q * n_rows);
-        rtamd::JitterPlan& plan = ws.jplan[K];
-        const int levels = rtamd::mt_levels_needed(K, q1);
-        if (plan.K != K || plan.levels < levels) {
-            try {
-                HIP_TRY(plan.build(K, levels));
-            } catch (const std::exception& ex) {
-                rtamd::set_last_error(std::string("jitter plan: ") + ex.what());
-                return RT_ERR_PROCESSING;
-            }
-        }
-        HIP_TRY(ws.ckpt.ensure(rtamd::mt_ckpt_words(K, q1) * sizeof(uint32_t)));
         HIP_TRY(ws.jit.ensure((size_t)n_rows * 16 * W * sizeof(double)));
-        HIP_TRY(ws.jscratch.ensure(rtamd::mt_scratch_bytes(K, ws.jranges)));
+        HIP_TRY(ws.jscratch.ensure(rtamd::mt_fill_scratch_bytes(ws.jranges)));
         HIP_TRY(upload(ws.rows, f->rows_jrow, st));
-        HIP_TRY(rtamd::mt_launch_jitter(plan, ws.jranges, ws.jjob, ws.jscratch.p, ws.ckpt.as<uint32_t>(),
-                                        ws.jit.as<double>(), st));
+        HIP_TRY(rtamd::mt_launch_fill(ws.jtab, ws.jranges, ws.jjob, ws.jscratch.p, ws.jit.as<double>(), st));
+        (void)q1;
     } else if (n_rows > 0) {
         // rows needing a primary hit: rendered rows and their vertical neighbours
         std::vector<char> need(H, 0), shade_row(H, 0);
@@ -707,10 +681,27 @@ extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
 
 extern "C" int rt_test_jitter_device(int K, int64_t q0, int64_t q1, int64_t first, int64_t count,
                                      double* out_host) {
-    if (K <= 0 || q0 < 0 || q1 <= q0 || (q0 & 1) || (q1 & 1) || !out_host || first * 2 < q0 || (first + count) * 2 > q1)
+    if (K < 0 || q0 < 0 || q1 <= q0 || (q0 & 1) || (q1 & 1) || !out_host || first * 2 < q0 || (first + count) * 2 > q1)
         return RT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
+    if (K == 0) {   // the frame path: checkpoint table + one-wave fill
+        rtamd::JitterTable T;
+        HIP_TRY(T.ensure((q1 - 1) / ((int64_t)rtamd::kTableK * 624) + 1, nullptr));
+        DBuf dj, ds;
+        const std::vector<rtamd::JRange> ranges{rtamd::JRange{q0, q1, 0}};
+        rtamd::JitterJob job;
+        HIP_TRY(dj.ensure((size_t)(q1 - q0) / 2 * sizeof(double)));
+        HIP_TRY(ds.ensure(rtamd::mt_fill_scratch_bytes(ranges)));
+        HIP_TRY(rtamd::mt_launch_fill(T, ranges, job, ds.p, dj.as<double>(), nullptr));
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(out_host, dj.as<double>() + (first - q0 / 2), (size_t)count * sizeof(double),
+                          hipMemcpyDeviceToHost));
+        T.release();
+        (void)hipFree(dj.p);
+        (void)hipFree(ds.p);
+        return RT_OK;
+    }
     rtamd::JitterPlan plan;
     HIP_TRY(plan.build(K, rtamd::mt_levels_needed(K, q1)));
     DBuf dc, dj, ds;
@@ -728,6 +719,46 @@ extern "C" int rt_test_jitter_device(int K, int64_t q0, int64_t q1, int64_t firs
     (void)hipFree(dj.p);
     (void)hipFree(ds.p);
     return RT_OK;
+}
+
+extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32_t* out) {
+    if (!s || !out) return RT_ERR_INVALID_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
+    try {
+        const rt_scene_desc& d = *rt_scene_get_desc(s);
+        const rtamd::CompiledScene cs = rtamd::compile_scene(d);
+        bool secondary = false;
+        for (int i = 0; i < d.n_materials; ++i)
+            if (d.materials[i].kr > 0.0 || d.materials[i].kt > 0.0) secondary = true;
+        if (d.recursion_limit < 2) secondary = false;
+        const bool deep = cs.max_ivl_depth > 2 || d.n_dir_lights > 0;
+        int n_bounded = 0;
+        for (const auto& o : cs.objs)
+            if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
+        const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
+        const bool f32 = (flags & RT_FLAG_FP32) != 0;
+        const void* fn = mode == RT_MODE_PAPER
+                             ? (f32 ? rtf::paper_kernel(cs.has_eager, deep, wv) : rtd::paper_kernel(cs.has_eager, deep, wv))
+                             : (f32 ? rtf::std_kernel(cs.has_eager, deep, secondary, wv)
+                                    : rtd::std_kernel(cs.has_eager, deep, secondary, wv));
+        hipFuncAttributes a{};
+        HIP_TRY(hipFuncGetAttributes(&a, fn));
+        int blocks = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0));
+        out[0] = a.numRegs;                      // VGPRs per lane
+        out[1] = (int32_t)a.localSizeBytes;      // scratch (spill) bytes per lane
+        out[2] = (int32_t)a.sharedSizeBytes;     // static LDS per workgroup
+        out[3] = blocks;                         // resident 256-thread workgroups per CU
+        out[4] = blocks * 4 / 4;                 // waves per SIMD (4 waves per workgroup, 4 SIMDs per CU)
+        out[5] = a.maxThreadsPerBlock;
+        out[6] = wv ? 1 : 0;
+        out[7] = secondary ? 1 : 0;
+        return RT_OK;
+    } catch (const std::exception& e) {
+        rtamd::set_last_error(std::string("scene compile: ") + e.what());
+        return RT_ERR_INVALID_ARG;
+    }
 }
 
 extern "C" int rt_test_compile_info(const rt_scene* s, int32_t* out) {

@@ -152,3 +152,23 @@ def test_frame_chunks_on_two_streams(gpu, mode):
                                    C.c_void_p(buf2.data_ptr()), None, C.byref(st1))
     assert rc == 0
     assert (st.rays_intersect, st.rays_occluded) == (st1.rays_intersect, st1.rays_occluded)
+
+
+TSEG = 64 * 624   # checkpoint-table segment (rtamd::kTableK twist blocks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q0,q1,first,count", [
+    (0, 3 * TSEG, 0, 4096),                                  # first draws, first table segments
+    (0, 6 * TSEG, TSEG // 2 - 100, 400),                     # across a segment start
+    (7 * TSEG - 64, 9 * TSEG + 4096, 7 * TSEG // 2 - 32, 2048),   # range starting mid-segment
+    (FRAME_4K - 32 * 3840 * 3, FRAME_4K, FRAME_4K // 2 - 16 * 3840 * 3, 16 * 3840 * 3),   # last rows of 4K
+    (FRAME_8K - 64, FRAME_8K, FRAME_8K // 2 - 32, 32),       # last pixels of 8K (table of 26.6k checkpoints)
+])
+def test_jitter_table_path_matches_serial(gpu, q0, q1, first, count):
+    """The frame path (K = 0 in the hook): resident checkpoint table every 64
+    twist blocks + the one-wavefront fill kernel, draw for draw against the
+    serial stream."""
+    dev = _device_draws(q0, q1, first, count, K=0)
+    ref = _oracle_draws(first, count)
+    assert np.array_equal(dev, ref)

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Render `--frames` frames of a bench config through the product path
+(rt_render_dist, world 1) and exit.  The program bench.py runs under
+rocprofv3 --pmc to measure the trace kernel's HBM traffic (one counter per
+pass), so that the traffic in the bench line is measured in the same run."""
+import argparse
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=4)
+    ap.add_argument("--frames", type=int, default=2)
+    ap.add_argument("--flags", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+
+    import rtamd
+    import scenes
+
+    text, mode = scenes.config_json(a.config)
+    sc = rtamd.load_scene_from_json_text(text)
+    W, H = sc.width, sc.height
+    lib = rtamd.amd_lib()
+    uid = (C.c_uint8 * 128)()
+    d = C.c_void_p()
+    if lib.rt_dist_get_id(uid) != 0 or lib.rt_dist_create(uid, 1, 0, C.byref(d)) != 0:
+        raise RuntimeError(rtamd.last_error())
+    out = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    st = rtamd.Stats()
+    for _ in range(a.frames):
+        if lib.rt_render_dist(d, sc.handle, W, H, mode, a.flags, C.c_void_p(out.data_ptr()), None, C.byref(st)) != 0:
+            raise RuntimeError(rtamd.last_error())
+    torch.cuda.synchronize()
+    lib.rt_dist_destroy(d)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
