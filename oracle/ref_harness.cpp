@@ -25,6 +25,7 @@
 
 #include "oracle.h"
 #include "rt.h"
+#include "rt_ref_adapter.hpp"
 
 static uint64_t g_n_isect = 0, g_n_occl = 0;
 
@@ -155,6 +156,17 @@ void export_hit(const Built& b, const Hit& h, oracle_hit* o) {
 }  // namespace
 
 extern "C" {
+
+// The reference-side binding (integration/rt_ref_adapter.cpp): IR -> the
+// reference's own objects -> rtref::scene_from_reference -> a new rt_scene.
+// Tests compare it with the input IR (tests/test_ref_adapter.py).
+int ref_roundtrip(const rt_scene_desc* d, void** out_scene) {
+    auto b = build(d);
+    rt_scene* s = nullptr;
+    const int rc = rtref::scene_from_reference(b->scene, b->cam, &s);
+    *out_scene = s;
+    return rc;
+}
 
 // Tracer::render (tracer.cpp:247-305) on the full frame.
 int ref_render(const rt_scene_desc* d, int W, int H, int mode, double* fb, uint64_t* n_isect, uint64_t* n_occl) {

@@ -218,6 +218,8 @@ def ref_lib():
                                        _dp, _dp]
         lib.ref_jitter.argtypes = [C.c_uint64, C.c_uint64, _dp]
         lib.ref_mt_words.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
+        if hasattr(lib, "ref_roundtrip"):
+            lib.ref_roundtrip.argtypes = [C.POINTER(SceneDesc), C.POINTER(C.c_void_p)]
         _ref = lib
     return _ref
 

@@ -1,11 +1,18 @@
 #!/usr/bin/env python3
 """Per-rank cost of the multi-GPU row split, measured on ONE GPU (GPU box).
 
-For each world size N, every rank's share of the frame (frame_dist.strip_rows)
-is rendered in turn on cuda:0 and timed (host wall clock around the blocking
-rt_render_rows_device call, plus the library's own HIP-event split into
-jitter stream and trace kernel).  The slowest rank bounds the N-GPU step
-before the gather; the gather itself is not simulated here.
+For each world size N, every rank's share of the frame (rt_dist_rows: the
+partition rt_render_dist uses) is rendered in turn on cuda:0 through
+rt_frame_* in the product's 4 row chunks and timed (host wall clock around
+the blocking call, plus the library's HIP-event split into jitter stream and
+trace kernel).  The slowest rank bounds the N-GPU step before the gather.
+
+The gather is added as a model: chunks 1..3 of a rank are gathered while the
+next chunk traces, so the exposed part is the LAST chunk's ncclGather into
+rank 0 (N-1 peers, each on its own xGMI link, in parallel) plus its
+placement on the root; a link is priced at 64 GB/s (conservative) and 153
+GB/s (the per-link figure of the MI355X spec sheet), the placement at the
+measured device copy rate of the same bytes.
 
 Usage: python tools/sim_ranks.py [--config 4] [--worlds 1,2,4,8] [--reps 3]
 """
@@ -32,7 +39,8 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--strip", type=int, default=frame_dist.STRIP)
-    ap.add_argument("--chunks", type=int, default=1, help="trace through rt_frame_* in this many chunks")
+    ap.add_argument("--chunks", type=int, default=4, help="trace through rt_frame_* in this many chunks")
+    ap.add_argument("--rgb8", action="store_true", help="gather 3 B/px (the CLI path) instead of FP64")
     ap.add_argument("--two-streams", action="store_true", help="alternate chunks between two streams")
     args = ap.parse_args()
     text, mode = scenes.config_json(args.config)
@@ -65,7 +73,7 @@ def main():
     for N in [int(v) for v in args.worlds.split(",")]:
         per = []
         for r in range(N):
-            rows = frame_dist.strip_rows(H, r, N, args.strip)
+            rows = rtamd.dist_rows(H, N, r) if args.strip == frame_dist.STRIP else frame_dist.strip_rows(H, r, N, args.strip)
             run(rows)
             wall, rng, ker = [], [], []
             for _ in range(args.reps):
@@ -81,11 +89,30 @@ def main():
         worst = max(p["wall_ms"] for p in per)
         if base is None and N == 1:
             base = worst
+        # exposed gather of the last chunk (model) + its placement on the root (measured copy rate)
+        m = max(p["rows"] for p in per)
+        bpp = 3 if args.rgb8 else 24
+        last_chunk = (m - (args.chunks - 1) * m // args.chunks) * W * bpp
+        src = torch.empty(max(1, last_chunk * N), dtype=torch.uint8, device="cuda")
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        for _ in range(5):
+            dst.copy_(src)
+        torch.cuda.synchronize()
+        place_ms = (time.perf_counter() - tc) / 5 * 1e3 if N > 1 else 0.0
+        g64 = (last_chunk / 64e9 * 1e3 + place_ms) if N > 1 else 0.0
+        g153 = (last_chunk / 153e9 * 1e3 + place_ms) if N > 1 else 0.0
         out = {"config": args.config, "world": N, "strip": args.strip, "chunks": args.chunks, "two_streams": args.two_streams, "max_rank_wall_ms": round(worst, 3),
                "max_rank_rng_ms": round(max(p["rng_ms"] for p in per), 3),
                "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
                "min_rank_kernel_ms": round(min(p["kernel_ms"] for p in per), 3),
-               "speedup_before_gather": round(base / worst, 3) if base else None}
+               "speedup_before_gather": round(base / worst, 3) if base else None,
+               "gather_bytes_per_rank": m * W * bpp, "exposed_gather_ms_64GBs": round(g64, 3),
+               "exposed_gather_ms_153GBs": round(g153, 3),
+               "projected_speedup_64GBs": round(base / (worst + g64), 3) if base else None,
+               "projected_speedup_153GBs": round(base / (worst + g153), 3) if base else None}
         print(json.dumps(out), flush=True)
 
 
