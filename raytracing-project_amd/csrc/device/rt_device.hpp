@@ -53,9 +53,15 @@ __device__ __forceinline__ float fabs_r(float x) { return __builtin_fabsf(x); }
 
 constexpr real kEPS = RV(1e-6);   // core.h:10
 
+#ifdef RT_BIG_STACKS
+constexpr int kMaxDepth = rtamd::kBigDepth;
+constexpr int kMaxIvlSpill = rtamd::kBigIvlSpill;
+constexpr int kMaxRayStack = rtamd::kBigRayStack;
+#else
 using rtamd::kMaxDepth;
 using rtamd::kMaxIvlSpill;
 using rtamd::kMaxRayStack;
+#endif
 
 struct V3 {
     real x, y, z;

@@ -312,6 +312,13 @@ void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const 
 void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const SceneView& V,
                 const StdParams& P) {
     const DevScene S = make_scene(V);
+#ifdef RT_GENERAL_ONLY
+    // big-stack build: only the general variants (every feature, scratch stacks)
+    (void)e;
+    (void)d;
+    if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
+    else launch_std_c<true, true, false>(c, grid, st, S, P);
+#else
     const bool wv = V.cull && V.n_bounded >= 4;
     if (e) {
         if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
@@ -331,10 +338,16 @@ void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, con
             else hipLaunchKernelGGL((k_std_lean<false, false>), grid, dim3(256), 0, st, S, P);
         }
     }
+#endif
 }
 
 void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const SceneView& V, const PaperParams& P) {
     const DevScene S = make_scene(V);
+#ifdef RT_GENERAL_ONLY
+    (void)e;
+    (void)d;
+    launch_paper_c<true, true>(c, grid, st, S, P);
+#else
     const bool wv = V.cull && V.n_bounded >= 4;
     if (e) launch_paper_c<true, true>(c, grid, st, S, P);
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
@@ -345,20 +358,31 @@ void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const Scene
         if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, false>), grid, dim3(256), 0, st, S, P);
         else hipLaunchKernelGGL((k_paper_primary_lean<false, false>), grid, dim3(256), 0, st, S, P);
     }
+#endif
 }
 
 // The kernel launch_std / launch_paper pick for a variant (resource queries).
 const void* std_kernel(bool e, bool d, bool sec, bool wv) {
+#ifdef RT_GENERAL_ONLY
+    (void)e, (void)d, (void)wv;
+    return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
+#else
     if (e) return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
     if (d) return sec ? (const void*)k_std<false, true, true, false> : (const void*)k_std<false, true, false, false>;
     if (sec) return wv ? (const void*)k_std<false, false, true, false, true> : (const void*)k_std<false, false, true, false>;
     return wv ? (const void*)k_std_lean<false, true> : (const void*)k_std_lean<false, false>;
+#endif
 }
 
 const void* paper_kernel(bool e, bool d, bool wv) {
+#ifdef RT_GENERAL_ONLY
+    (void)e, (void)d, (void)wv;
+    return (const void*)k_paper_primary<true, true, false>;
+#else
     if (e) return (const void*)k_paper_primary<true, true, false>;
     if (d) return (const void*)k_paper_primary<false, true, false>;
     return wv ? (const void*)k_paper_primary_lean<false, true> : (const void*)k_paper_primary_lean<false, false>;
+#endif
 }
 
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {

@@ -109,9 +109,16 @@ struct PaperParams {
     unsigned long long* counters;
 };
 
-constexpr int kMaxRayStack = 8;   // transform nesting (checked on the host)
-constexpr int kMaxIvlSpill = 6;   // interval stack entries beyond the top two
-constexpr int kMaxDepth = 16;     // recursion frames (medium.recursion <= 16)
+// Per-lane stacks of the render kernels (checked on the host per scene).
+// The common kernels carry small ones; scenes beyond them run on the
+// "big-stack" build of the general kernels (namespace rtdb,
+// rt_kernels_big.hip), whose stacks live in scratch memory.
+constexpr int kMaxRayStack = 8;   // transform nesting inside CSG operands (eager programs)
+constexpr int kMaxIvlSpill = 6;   // CSG interval stack entries beyond the top two
+constexpr int kMaxDepth = 16;     // reflection/refraction frames (medium.recursion <= 17)
+constexpr int kBigRayStack = 64;
+constexpr int kBigIvlSpill = 62;
+constexpr int kBigDepth = 128;    // medium.recursion <= 129
 
 constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
 constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics
@@ -133,3 +140,4 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
     }
 RT_DECLARE_LAUNCHERS(rtd)
 RT_DECLARE_LAUNCHERS(rtf)
+RT_DECLARE_LAUNCHERS(rtdb)

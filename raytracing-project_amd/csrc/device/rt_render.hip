@@ -154,6 +154,7 @@ struct rt_frame {
     SceneView S;
     int W = 0, H = 0, mode = 0, n_rows = 0;
     bool eager = false, deep = false, secondary = false, count_ops = false, fp32 = false;
+    bool big = false;                          // big-stack kernels (rtdb)
     bool traced = false;
     std::vector<int32_t> rows;
     std::vector<int32_t> rows_jrow;            // standard mode: rows | jitter row of each
@@ -288,17 +289,29 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         sc.valid = true;
     }
     const rtamd::CompiledScene& cs = sc.cs;
-    if (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2) {
-        rtamd::set_last_error("scene nesting exceeds the device stacks (transforms <= 8, CSG operand depth <= 8)");
-        return RT_ERR_UNSUPPORTED;
-    }
     bool secondary = false;
     for (int i = 0; i < d.n_materials; ++i)
         if (d.materials[i].kr > 0.0 || d.materials[i].kt > 0.0) secondary = true;
     if (d.recursion_limit < 2) secondary = false;   // depth < limit-1 never holds (tracer.cpp:38,51)
-    if (secondary && mode == RT_MODE_STANDARD && d.recursion_limit - 1 > kMaxDepth) {
-        rtamd::set_last_error("medium.recursion exceeds the device frame stack (17)");
-        return RT_ERR_UNSUPPORTED;
+    // Stack tiers: the common kernels, else the big-stack build (rtdb), else refuse.
+    const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
+    bool big = false;
+    if (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2 || frames > kMaxDepth) {
+        if (cs.max_ray_depth > rtamd::kBigRayStack || cs.max_ivl_depth > rtamd::kBigIvlSpill + 2 ||
+            frames > rtamd::kBigDepth) {
+            rtamd::set_last_error("scene exceeds the device stacks: transform nesting inside CSG operands " +
+                                  std::to_string(cs.max_ray_depth) + " (max " + std::to_string(rtamd::kBigRayStack) +
+                                  "), CSG operand depth " + std::to_string(cs.max_ivl_depth) + " (max " +
+                                  std::to_string(rtamd::kBigIvlSpill + 2) + "), medium.recursion " +
+                                  std::to_string(d.recursion_limit) + " with reflection/refraction (max " +
+                                  std::to_string(rtamd::kBigDepth + 1) + ")");
+            return RT_ERR_UNSUPPORTED;
+        }
+        if (fp32) {
+            rtamd::set_last_error("the FP32 fast path has only the common device stacks; render this scene in FP64");
+            return RT_ERR_UNSUPPORTED;
+        }
+        big = true;
     }
     f->st = st;
     f->W = W;
@@ -312,6 +325,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->secondary = secondary;
     f->count_ops = (flags & RT_FLAG_COUNT_OPS) != 0;
     f->fp32 = fp32;
+    f->big = big;
     f->rows.assign(rows_host, rows_host + n_rows);
     f->t_start = t_start;
     if (!ws.ev[0])
@@ -459,6 +473,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         P.counters = ctr;
         dim3 grid((W + 7) / 8, (n + 3) / 4);
         if (f->fp32) rtf::launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
+        else if (f->big) rtdb::launch_std(true, true, f->secondary, f->count_ops, grid, st, f->S, P);
         else rtd::launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
         HIP_TRY(hipGetLastError());
     } else {
@@ -507,6 +522,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
             HIP_TRY(hipMemcpyAsync(d_list, L.data(), L.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
             dim3 g1((W + 15) / 16, (P.n_list + 15) / 16);
             if (f->fp32) rtf::launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
+            else if (f->big) rtdb::launch_paper(true, true, f->count_ops, g1, st, f->S, P);
             else rtd::launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
             HIP_TRY(hipGetLastError());
         }
@@ -738,7 +754,12 @@ extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32
             if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
         const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
         const bool f32 = (flags & RT_FLAG_FP32) != 0;
-        const void* fn = mode == RT_MODE_PAPER
+        const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
+        const bool big = !f32 && (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2 ||
+                                  frames > kMaxDepth);
+        const void* fn = big ? (mode == RT_MODE_PAPER ? rtdb::paper_kernel(true, true, false)
+                                                      : rtdb::std_kernel(true, true, secondary, false))
+                       : mode == RT_MODE_PAPER
                              ? (f32 ? rtf::paper_kernel(cs.has_eager, deep, wv) : rtd::paper_kernel(cs.has_eager, deep, wv))
                              : (f32 ? rtf::std_kernel(cs.has_eager, deep, secondary, wv)
                                     : rtd::std_kernel(cs.has_eager, deep, secondary, wv));

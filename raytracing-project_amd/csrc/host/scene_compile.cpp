@@ -402,10 +402,8 @@ public:
                 o.kind = OBJ_CHAIN;
                 o.m = (int)chain.size();
                 rdepth_ = idepth_ = 0;
-                for (int t : chain) {
-                    op(OP_XPUSH, t, 0);
-                    ray_push();
-                }
+                // (a chain maps its ray level by level in registers: no ray stack)
+                for (int t : chain) op(OP_XPUSH, t, 0);
                 o.node = core;
                 o.cpc0 = (int)cs.ops.size();
                 if (leaf_core) {

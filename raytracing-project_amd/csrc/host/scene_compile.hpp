@@ -89,7 +89,7 @@ struct CompiledScene {
     std::vector<FoldLeaf> fold;    // leaves of the fold objects (DevObj::fold0)
     std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated;
                                    // then the leaf prefilter balls of CHAIN objects (world frame, see DevObj::pb0)
-    int max_ray_depth = 0;   // transform nesting on any path
+    int max_ray_depth = 0;   // transform nesting on any path of an eager program (chains need no stack)
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter
     bool has_pokeball = false;

@@ -294,6 +294,64 @@ def torture_scenes(dpi: int = 24) -> dict[str, dict]:
     return sc
 
 
+def deep_scenes(dpi: int = 12) -> dict[str, dict]:
+    """Valid scenes beyond the common kernels' stacks (rt_launch.hpp): the
+    reference recurses without a limit through trace_recursive
+    (tracer.cpp:22-73), the transform wrappers (transform.cpp:18-255) and
+    binary csg nodes (json_loader.cpp:354-366); the device runs these on its
+    big-stack kernels.
+      mirrors_rec24   reflective floor + ceiling, medium.recursion 24 (23 frames)
+      xform_nest12    a sphere under 12 nested transforms inside a CSG operand
+                      (eager program, ray stack 12) and as a bare chain
+      csg_right12     a 12-leaf right-nested binary csg (interval stack 12)"""
+    lights = [{"position": [0.0, 1.0, 2.0], "intensity": [6, 6, 6]},
+              {"position": [-1.5, 0.5, -1.0], "intensity": [4, 3, 3]}]
+    sc = {}
+    sc["mirrors_rec24"] = _base([
+        {"halfSpace": {"position": [0, -1.2, 0], "normal": [0, 1, 0],
+                       "color": _mat([0.2, 0.3, 0.2], reflected=[0.85, 0.85, 0.85])}},
+        {"halfSpace": {"position": [0, 1.6, 0], "normal": [0, -1, 0],
+                       "color": _mat([0.3, 0.2, 0.2], reflected=[0.8, 0.8, 0.8])}},
+        {"sphere": {"position": [-0.8, 0.0, -1.5], "radius": 0.6, "color": _mat([0.8, 0.5, 0.2])}},
+        {"sphere": {"position": [0.9, 0.2, -2.0], "radius": 0.5, "index": 1.4,
+                    "color": _mat([0.1, 0.1, 0.3], refracted=[0.8, 0.8, 0.8])}},
+    ], recursion=24, dpi=dpi, lights=lights)
+
+    def nest(leaf, n):
+        node = leaf
+        for k in range(n):
+            if k % 3 == 0:
+                node = {"translation": {"factors": [0.03 * (1 - 2 * (k % 2)), 0.02, 0.0], "subject": node}}
+            elif k % 3 == 1:
+                node = {"rotation": {"angle": 8 + k, "direction": k % 3, "subject": node}}
+            else:
+                node = {"scaling": {"factors": [1.03, 0.97, 1.01], "subject": node}}
+        return node
+
+    sc["xform_nest12"] = _base([
+        {"halfSpace": {"position": [0, -1.2, 0], "normal": [0, 1, 0], "color": _mat([0.5, 0.6, 0.5])}},
+        {"union": [nest({"sphere": {"position": [-0.9, 0.0, -1.0], "radius": 0.6, "color": _mat([0.8, 0.3, 0.3])}},
+                        12),
+                   {"sphere": {"position": [-0.2, 0.5, -1.4], "radius": 0.4, "color": _mat([0.3, 0.3, 0.8])}}]},
+        nest({"sphere": {"position": [1.0, 0.0, -1.2], "radius": 0.5, "color": _mat([0.3, 0.8, 0.3])}}, 12),
+    ], dpi=dpi)
+
+    def right_nested(leaves, ops):
+        node = leaves[-1]
+        for leaf, op in zip(reversed(leaves[:-1]), reversed(ops)):
+            node = {"csg": {"operator": op, "left": leaf, "right": node}}
+        return node
+
+    leaves = [{"sphere": {"position": [-1.6 + 0.3 * i, 0.25 * math.sin(i), -1.2 - 0.1 * i], "radius": 0.35 + 0.02 * i,
+                          "color": _mat([0.2 + 0.06 * i, 0.8 - 0.05 * i, 0.4])}} for i in range(12)]
+    ops = ["union"] * 5 + ["difference"] + ["union"] * 3 + ["intersection"] + ["union"]
+    sc["csg_right12"] = _base([
+        {"halfSpace": {"position": [0, -1.2, 0], "normal": [0, 1, 0], "color": _mat([0.5, 0.6, 0.5])}},
+        right_nested(leaves, ops),
+    ], dpi=dpi)
+    return sc
+
+
 def dir_light_cases(dpi: int = 16) -> dict[str, tuple[str, list]]:
     """Scenes with directional lights (the reference's Scene::dir_lights,
     scene.h:10-15; its loader never creates them, so they are attached to the

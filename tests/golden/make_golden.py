@@ -15,8 +15,11 @@ turned into IR by our loader (librt_host.so).  Outputs are data only:
   cameras.npz  Camera::generate_ray / generate_ray_subpixel outputs
   dirlights.npz  frames + counts of scenes with directional lights attached
                (scenes.dir_light_cases), standard and paper mode
+  deep.npz     frames + counts of the scenes beyond the device's common
+               stacks (scenes.deep_scenes: recursion 24, 12 nested
+               transforms, a 12-leaf right-nested csg), both modes
 
-Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights]
+Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights deep]
 """
 from __future__ import annotations
 
@@ -75,6 +78,21 @@ def make_frames():
             data[f"{name}/scene"] = np.frombuffer(text.encode(), dtype=np.uint8)
     np.savez_compressed(os.path.join(HERE, "frames.npz"), **data)
     print("frames:", len(data))
+
+
+def make_deep():
+    data = {}
+    for name, d in scenes.deep_scenes(dpi=12).items():
+        text = json.dumps(d)
+        sc = rtamd.load_scene_from_json_text(text)
+        for mode in (0, 1):
+            with quiet_stdout():
+                fb, ni, no = rtamd.ref_render(sc, sc.width, sc.height, mode)
+            data[f"{name}/{mode}/fb"] = fb
+            data[f"{name}/{mode}/counts"] = np.array([ni, no], dtype=np.int64)
+        data[f"{name}/scene"] = np.frombuffer(text.encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "deep.npz"), **data)
+    print("deep:", len(data))
 
 
 def _random_rays(rng, n, center, spread):
@@ -194,3 +212,4 @@ if __name__ == "__main__":
     make_jitter()
     make_cameras()
     make_dirlights()
+    make_deep()

@@ -268,3 +268,19 @@ def test_oracle_dir_lights_bit_exact(rt, mode):
         assert np.array_equal(fb, gold[f"{name}/{mode}/fb"]), name
         cnt = gold[f"{name}/{mode}/counts"]
         assert (st.rays_intersect, st.rays_occluded) == (int(cnt[0]), int(cnt[1])), name
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_oracle_deep_scenes_bit_exact(rt, mode):
+    """Scenes beyond the device's common stacks (scenes.deep_scenes:
+    recursion 24, 12 nested transforms, a 12-leaf right-nested csg) against
+    frames of the reference itself (tests/golden/deep.npz, make_golden.py)."""
+    fr = np.load(os.path.join(GOLDEN, "deep.npz"))
+    names = _scene_names(fr)
+    assert set(names) == {"mirrors_rec24", "xform_nest12", "csg_right12"}
+    for name in names:
+        sc = rt.load_scene_from_json_text(bytes(fr[f"{name}/scene"]).decode())
+        fb, st = rt.oracle_render(sc, sc.width, sc.height, mode, threads=4)
+        assert np.array_equal(fb, fr[f"{name}/{mode}/fb"]), name
+        cnt = fr[f"{name}/{mode}/counts"]
+        assert (st.rays_intersect, st.rays_occluded) == (int(cnt[0]), int(cnt[1])), name
