@@ -1656,9 +1656,14 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
 // 0..1023 x^k is evaluated by left-to-right binary powering in double-double
 // arithmetic (exact products by fma, ~2^-100 relative error), and rounded
 // once: the correctly rounded x^k.  Other exponents use the library pow.
+// The library pow for non-integer exponents (no reference scene has one) is
+// kept out of line: inlined, its temporaries set the trace kernel's register
+// peak and made the compiler spill ~130 B/lane on the common integer path.
+__device__ __attribute__((noinline)) double pow_general(double x, double y) { return pow(x, y); }
+
 __device__ __forceinline__ double pow_spec(double x, double y) {
     const int k = (int)y;
-    if (!(y >= 0.0 && y < 1024.0 && (double)k == y)) return pow(x, y);
+    if (!(y >= 0.0 && y < 1024.0 && (double)k == y)) return pow_general(x, y);
     if (k == 0) return 1.0;   // pow(x, 0) = 1 for every x
     const int top = 31 - __builtin_clz(k);
     double h = x, l = 0.0;

@@ -28,14 +28,24 @@ namespace {
 // then one atomic per block and counter into one of kCounterSlots slots
 // (blockIdx-hashed).  A single hot address would serialize ~2M atomics at the
 // L2 (~6 ns each, MI355X_MICROARCH.md fan-in row) - 12 ms per 4K frame.
-template <bool C>
+// Standard-mode workgroup: RT_STD_WPB waves of 4x2 pixels x 8 samples
+// (default 4: 8x4 pixels per 256-thread workgroup).
+#ifndef RT_STD_WPB
+#define RT_STD_WPB 4
+#endif
+constexpr int kStdWPB = RT_STD_WPB;
+constexpr int kStdThreads = 64 * kStdWPB;
+constexpr int kStdBlockX = kStdWPB >= 2 ? 8 : 4;            // pixels per workgroup in x
+constexpr int kStdBlockY = kStdWPB >= 4 ? 4 : 2;            // output rows per workgroup
+
+template <bool C, int NWAVES = 4>
 __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
 #ifdef RT_PHASE_PROF
     constexpr int NW = C ? 18 : 2 + PH_COUNT;
 #else
     constexpr int NW = C ? 18 : 2;
 #endif
-    __shared__ unsigned long long red[4][NW];
+    __shared__ unsigned long long red[NWAVES][NW];
     unsigned long long v[NW];
     v[0] = ni;
     v[1] = no;
@@ -57,10 +67,11 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
     if (lane == 0)
 #pragma unroll
         for (int k = 0; k < NW; ++k) red[wave][k] = v[k];
-    __syncthreads();
+    if constexpr (NWAVES > 1) __syncthreads();
     if (threadIdx.x < NW) {
-        const unsigned long long sum = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                       red[3][threadIdx.x];
+        unsigned long long sum = 0;
+#pragma unroll
+        for (int w = 0; w < NWAVES; ++w) sum += red[w][threadIdx.x];
         const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x) % kCounterSlots;
         if (sum) atomicAdd(&ctr[(size_t)slot * kCounterWords + threadIdx.x], sum);
     }
@@ -80,8 +91,8 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     const int wave = threadIdx.x >> 6;
     const int s = lane & 7;
     const int pix = lane >> 3;
-    const int x = blockIdx.x * 8 + (wave & 1) * 4 + (pix & 3);
-    const int ri = blockIdx.y * 4 + (wave >> 1) * 2 + (pix >> 2);
+    const int x = blockIdx.x * kStdBlockX + (wave & 1) * 4 + (pix & 3);
+    const int ri = blockIdx.y * kStdBlockY + (wave >> 1) * 2 + (pix >> 2);
     const bool active = x < P.W && ri < P.n_rows;
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
@@ -118,18 +129,18 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
         o[2] = acc.z * inv;
     }
     cnt.pe(PH_TAIL);
-    flush_counters(P.counters, ni, no, cnt);
+    flush_counters<C, kStdWPB>(P.counters, ni, no, cnt);
 }
 
 // WV: wave-level culling (scene_occluded_wave / scene_intersect_wave), picked
 // by the host for scenes with >= 4 bounded objects and culling on.
 template <bool E, bool D, bool SEC, bool C, bool WV = false>
-__global__ __launch_bounds__(256) void k_std(DevScene S, StdParams P) {
+__global__ __launch_bounds__(kStdThreads) void k_std(DevScene S, StdParams P) {
     std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
 template <bool C, bool WV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
+__global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
                                                                                                        StdParams P) {
     std_body<false, false, false, C, false, WV>(S, P);
 }
@@ -296,8 +307,8 @@ DevScene make_scene(const SceneView& V) {
 
 template <bool E, bool D, bool SEC, bool WV = false>
 void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true, WV>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std<E, D, SEC, false, WV>), grid, dim3(256), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+    else hipLaunchKernelGGL((k_std<E, D, SEC, false, WV>), grid, dim3(kStdThreads), 0, st, S, P);
 }
 
 template <bool E, bool D>
@@ -309,9 +320,9 @@ void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const 
 }  // namespace
 
 // Eager scenes always use D.  Each variant gets its own register allocation.
-void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const SceneView& V,
-                const StdParams& P) {
+void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneView& V, const StdParams& P) {
     const DevScene S = make_scene(V);
+    const dim3 grid((P.W + kStdBlockX - 1) / kStdBlockX, (P.n_rows + kStdBlockY - 1) / kStdBlockY);
 #ifdef RT_GENERAL_ONLY
     // big-stack build: only the general variants (every feature, scratch stacks)
     (void)e;
@@ -331,11 +342,11 @@ void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, con
             if (wv) launch_std_c<false, false, true, true>(c, grid, st, S, P);
             else launch_std_c<false, false, true>(c, grid, st, S, P);
         } else if (wv) {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, true>), grid, dim3(256), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, true>), grid, dim3(256), 0, st, S, P);
+            if (c) hipLaunchKernelGGL((k_std_lean<true, true>), grid, dim3(kStdThreads), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, true>), grid, dim3(kStdThreads), 0, st, S, P);
         } else {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, false>), grid, dim3(256), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, false>), grid, dim3(256), 0, st, S, P);
+            if (c) hipLaunchKernelGGL((k_std_lean<true, false>), grid, dim3(kStdThreads), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, false>), grid, dim3(kStdThreads), 0, st, S, P);
         }
     }
 #endif

@@ -130,7 +130,7 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
 // SEC = reflection/refraction frames, C = op counting.
 #define RT_DECLARE_LAUNCHERS(NS)                                                                                  \
     namespace NS {                                                                                                \
-    void launch_std(bool e, bool d, bool sec, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,      \
+    void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const rtamd::SceneView& V,                 \
                     const rtamd::StdParams& P);                                                                   \
     void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,               \
                       const rtamd::PaperParams& P);                                                               \

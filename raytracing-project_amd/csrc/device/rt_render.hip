@@ -471,10 +471,9 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         P.jit = ws.jit.as<double>();
         P.fb = fb;
         P.counters = ctr;
-        dim3 grid((W + 7) / 8, (n + 3) / 4);
-        if (f->fp32) rtf::launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
-        else if (f->big) rtdb::launch_std(true, true, f->secondary, f->count_ops, grid, st, f->S, P);
-        else rtd::launch_std(f->eager, f->deep, f->secondary, f->count_ops, grid, st, f->S, P);
+        if (f->fp32) rtf::launch_std(f->eager, f->deep, f->secondary, f->count_ops, st, f->S, P);
+        else if (f->big) rtdb::launch_std(true, true, f->secondary, f->count_ops, st, f->S, P);
+        else rtd::launch_std(f->eager, f->deep, f->secondary, f->count_ops, st, f->S, P);
         HIP_TRY(hipGetLastError());
     } else {
         // primary hits of the ext rows this chunk reads that no earlier chunk computed
