@@ -40,6 +40,12 @@ int rt_test_compile_info(const struct rt_scene* s, int32_t* out);
  * culling variant, reflection/refraction variant}.  Needs a device. */
 int rt_test_kernel_info(const struct rt_scene* s, int mode, int flags, int32_t* out);
 
+/* GPU: the shared-denominator division of the device code (rt_device.hpp
+ * div3) next to the compiler's own division on the same inputs:
+ * div3_host[3i+k] and plain_host[3i+k] = a[3i+k] / b[i].  Tests require the
+ * two to be bit-identical. */
+int rt_test_div3(const double* a_host, const double* b_host, int n, double* div3_host, double* plain_host);
+
 /* GPU, one device: the multi-GPU frame path of rt_render_multi /
  * rt_render_dist (partition, row chunks, gather stage layout, placement on
  * the root) with `world` simulated ranks rendered one after another on the

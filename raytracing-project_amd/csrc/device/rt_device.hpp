@@ -72,10 +72,50 @@ __device__ __forceinline__ real dmax(real a, real b) { return (a < b) ? b : a; }
 __device__ __forceinline__ real dmin(real a, real b) { return (b < a) ? b : a; }   // std::min
 __device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
 
+// (a0, a1, a2) / b: three IEEE divisions, bit-identical to the compiler's
+// own FP64 division (v_div_scale / v_rcp / two Newton steps / v_div_fmas /
+// v_div_fixup, the exact sequence `a / b` lowers to on gfx950), with the
+// reciprocal refinement done once when the scaled denominator is the same for
+// every numerator and lane (it depends on the numerator only at the extremes
+// of the exponent range, where the three divisions are done one by one).
+// tests/test_gpu_numerics.py checks it bit for bit against `/`.
+struct D3 {
+    double x, y, z;
+};
+__device__ __forceinline__ D3 div3(double a0, double a1, double a2, double b) {
+    bool u0, u1, u2;
+    const double s0 = __builtin_amdgcn_div_scale(a0, b, false, &u0);
+    const double s1 = __builtin_amdgcn_div_scale(a1, b, false, &u1);
+    const double s2 = __builtin_amdgcn_div_scale(a2, b, false, &u2);
+    const bool same = __double_as_longlong(s0) == __double_as_longlong(s1) &&
+                      __double_as_longlong(s0) == __double_as_longlong(s2);
+    if (!__all(same)) return D3{a0 / b, a1 / b, a2 / b};
+    const double rcp = __builtin_amdgcn_rcp(s0);
+    const double f0 = __builtin_fma(-s0, rcp, 1.0);
+    const double f1 = __builtin_fma(rcp, f0, rcp);
+    const double f2 = __builtin_fma(-s0, f1, 1.0);
+    const double f3 = __builtin_fma(f1, f2, f1);
+    auto quot = [&](double a) {
+        bool vcc;
+        const double n = __builtin_amdgcn_div_scale(a, b, true, &vcc);
+        const double mul = n * f3;
+        const double f4 = __builtin_fma(-s0, mul, n);
+        return __builtin_amdgcn_div_fixup(__builtin_amdgcn_div_fmas(f4, f3, mul, vcc), b, a);
+    };
+    return D3{quot(a0), quot(a1), quot(a2)};
+}
+__device__ __forceinline__ auto div3(float a0, float a1, float a2, float b) {
+    struct F3 { float x, y, z; };
+    return F3{a0 / b, a1 / b, a2 / b};
+}
+
 // Dir3::normalized (core.h:95-101)
 __device__ __forceinline__ V3 normalized(V3 v) {
     real L = sqrt_r(dot3(v, v));
-    if (L > kEPS) return v3(v.x / L, v.y / L, v.z / L);
+    if (L > kEPS) {
+        const auto q = div3(v.x, v.y, v.z, L);
+        return v3(q.x, q.y, q.z);
+    }
     return v3(RV(0.0), RV(1.0), RV(0.0));
 }
 
@@ -322,7 +362,8 @@ __device__ __forceinline__ int pick_region(const NodeT* nd, V3 p, CT& cnt) {
     cnt.inc(RT_OPC_POKE_REGION);
     const real* v = nd->v;
     const real r = v[3];
-    V3 u = v3((p.x - v[0]) / r, (p.y - v[1]) / r, (p.z - v[2]) / r);
+    const auto uq = div3(p.x - v[0], p.y - v[1], p.z - v[2], r);
+    V3 u = v3(uq.x, uq.y, uq.z);
     const real ang = acos(clamp1(dot3(u, v3(v[7], v[8], v[9]))));
     const real inner = dmax(RV(0.0), v[5] - v[6]);
     if (ang <= v[5]) return (ang >= inner) ? nd->mats[RT_PB_RING] : nd->mats[RT_PB_BUTTON];
@@ -1131,7 +1172,8 @@ __device__ __forceinline__ void leaf_shading(const NodeT* nd, const DRay& r, V3 
         return;
     }
     const real rad = nd->v[3];
-    const V3 outward = v3((p.x - nd->v[0]) / rad, (p.y - nd->v[1]) / rad, (p.z - nd->v[2]) / rad);
+    const auto oq = div3(p.x - nd->v[0], p.y - nd->v[1], p.z - nd->v[2], rad);
+    const V3 outward = v3(oq.x, oq.y, oq.z);
     set_face_normal(h, r, outward);
     h.mat = nd->kind == RT_NODE_SPHERE ? nd->mat : pick_region(nd, p, cnt);
 }
@@ -1758,7 +1800,8 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             real d2 = dot3(tl, tl);
             if (d2 <= RV(0.01)) d2 = RV(0.01);
             const real dist = sqrt_r(d2);
-            const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
+            const auto wq = div3(tl.x, tl.y, tl.z, dist);
+            const V3 wi = v3(wq.x, wq.y, wq.z);
             const real ndotl = dmax(RV(0.0), dot3(n, wi));
             const real max_t = dist - eps;
             // shading.cpp:86-103: back-facing lights and lights closer than
@@ -1795,7 +1838,8 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             real d2 = dot3(tl, tl);
             if (d2 <= RV(0.01)) d2 = RV(0.01);
             const real dist = sqrt_r(d2);
-            const V3 wi = v3(tl.x / dist, tl.y / dist, tl.z / dist);
+            const auto wq = div3(tl.x, tl.y, tl.z, dist);
+            const V3 wi = v3(wq.x, wq.y, wq.z);
             const real ndotl = dmax(RV(0.0), dot3(n, wi));
             cnt.inc(RT_OPC_SHADE_LIGHT);
             const real ed = dmax(RV(0.5), dist);
