@@ -179,7 +179,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         P.mat[idx] = hits ? h.mat : -3;
         if (P.ext_shade[ei]) {
             // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
-            V3 base = shade<E, D, DL, WV>(S, ht, h, normalized(vneg(r.d)), no, cnt, hits);
+            V3 base = shade<E, D, DL, WV, true>(S, ht, h, normalized(vneg(r.d)), no, cnt, hits);
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             P.lum[idx] = RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z;
         }
