@@ -1,0 +1,15 @@
+# Round-end evidence: full GPU suite, smoke, default bench line, and the
+# rocprofv3 kernel-trace summary of a short bench run (copied to profiles/ by hand: kernel_stats.csv, bench line, test tail).
+# Usage (GPU box): TAG=r02a bash tools/gpu/round.sh
+set -o pipefail
+export TMPDIR=/tmp
+T=${TAG:-r02}
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${T}_gpu_tests.log; exit 1; }
+tail -2 gpurun_out/${T}_gpu_tests.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/${T}_smoke.log; exit 1; }
+tail -1 gpurun_out/${T}_smoke.log
+timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { echo bench failed; tail gpurun_out/${T}_bench.err; exit 1; }
+tail -1 gpurun_out/${T}_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o run --output-format csv -- python bench.py --steps 50 --no-pmc --no-cpu --no-cli --fp32-steps 0 > gpurun_out/${T}_prof_bench.json 2>gpurun_out/${T}_prof.err || { echo prof failed; tail gpurun_out/${T}_prof.err; exit 1; }
+find gpurun_out/${T}_prof -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} gpurun_out/${T}_kernel_stats.csv
+head -8 gpurun_out/${T}_kernel_stats.csv
