@@ -177,12 +177,52 @@ enum RtPhase {
     PH_WAVE_SETUP,     // wave queries: bundle setup + transposed object test
     PH_COUNT
 };
+// Diagnostic builds with -DRT_EVENT_PROF instead count WAVE-level executions
+// of the events below (first active lane, so divergent paths count once per
+// wave that runs them) into rt_stats.ops[k]; no timers.
+enum RtEvent {
+    EV_SHQ = 0,        // shadow wave queries with some lane querying
+    EV_SH_CAND,        // shadow: candidate objects after the transposed test
+    EV_SH_HIT,         // shadow: object_hit calls (after the prefilters)
+    EV_SH_CSG,         //   of which CSG objects
+    EV_PR_CAND,        // primary: candidate objects
+    EV_PR_HIT,         // primary: object_hit calls
+    EV_FOLD_LEAF,      // fold_leaf_ivl executions
+    EV_COMB,           // csg_c executions past the both-empty test
+    EV_COMB_SINGLE,    //   one-operand path
+    EV_COMB_EASY,      //   union closed form
+    EV_COMB_GEN,       //   general sweep
+    EV_LIGHT1,         // light pass 1 iterations with some lane needing a query
+    EV_LIGHT2,         // light pass 2 iterations (lit lights)
+    EV_DIV3_SLOW,      // div3 one-by-one fallback
+    EV_COMPACT_LEAF,   // leaf_ivl_c executions
+    EV_WAVES,          // waves with an active lane
+    EV_COUNT
+};
 template <bool C>
 struct Cnt;
 template <>
 struct Cnt<false> {
     __device__ __forceinline__ void inc(int) {}
-#ifdef RT_PHASE_PROF
+#ifdef RT_EVENT_PROF
+    __device__ static unsigned long long* acc() {
+        __shared__ unsigned long long a[4][EV_COUNT];
+        return &a[threadIdx.x >> 6][0];
+    }
+    __device__ __forceinline__ void init() {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < EV_COUNT; ++k) acc()[k] = 0;
+    }
+    __device__ __forceinline__ bool first() {
+        return (int)__lane_id() == __builtin_ctzll(__builtin_amdgcn_read_exec());
+    }
+    __device__ __forceinline__ void ev(int k) {
+        if (first()) acc()[k] += 1;
+    }
+    __device__ __forceinline__ void pb(int) {}
+    __device__ __forceinline__ void pe(int) {}
+    __device__ __forceinline__ unsigned long long get(int k) { return acc()[k]; }
+#elif defined(RT_PHASE_PROF)
     // per-wave accumulators in LDS, updated by the first active lane, so
     // that phases inside divergent code are timed too (256-thread blocks)
     // (start stamps live in LDS too: no VGPRs taken from the kernel)
@@ -206,10 +246,12 @@ struct Cnt<false> {
         if (first()) acc()[k] += t - acc()[PH_COUNT + k];
     }
     __device__ __forceinline__ unsigned long long get(int k) { return acc()[k]; }
+    __device__ __forceinline__ void ev(int) {}
 #else
     __device__ __forceinline__ void init() {}
     __device__ __forceinline__ void pb(int) {}
     __device__ __forceinline__ void pe(int) {}
+    __device__ __forceinline__ void ev(int) {}
 #endif
 };
 template <>
@@ -220,6 +262,7 @@ struct Cnt<true> {
         for (int i = 0; i < 16; ++i) c[i] = 0;
     }
     __device__ __forceinline__ void inc(int k) { c[k]++; }
+    __device__ __forceinline__ void ev(int) {}
     __device__ __forceinline__ void init() {}
     __device__ __forceinline__ void pb(int) {}
     __device__ __forceinline__ void pe(int) {}
@@ -734,6 +777,7 @@ struct CIvl {
 // (geometry.cpp:48-78, 117-147, 207-217).
 template <class CT>
 __device__ __forceinline__ void leaf_ivl_c(const NodeT* nd, int pc, const DRay& r, CIvl& o, CT& cnt) {
+    cnt.ev(EV_COMPACT_LEAF);
     o.c0 = pc;
     o.c1 = pc | REF_ROOT1;
     if (nd->kind == RT_NODE_HALFSPACE) {
@@ -784,7 +828,9 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
     R.c0 = R.c1 = 0;
     if (!A.ok && !B.ok) return;
     cnt.inc(RT_OPC_CSG_COMBINE);
+    cnt.ev(EV_COMB);
     if (!(A.ok && B.ok)) {
+        cnt.ev(EV_COMB_SINGLE);
         // Exactly one operand has an interval X.  The sweep then sees only X's
         // events: an intersection is never inside; a difference without A is
         // never inside; otherwise the result is X itself, or, when the origin
@@ -829,6 +875,7 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
                           (fabs_r(A.t0 - B.t0) > e) && (fabs_r(A.t0 - B.t1) > e) && (fabs_r(A.t1 - B.t0) > e) &&
                           (fabs_r(A.t1 - B.t1) > e);
         if (easy) {
+            cnt.ev(EV_COMB_EASY);
             const bool inA = (A.t0 < e) && (A.t1 > e);
             const bool inB = (B.t0 < e) && (B.t1 > e);
             const bool xa = inA || (!inB && A.t0 < B.t0);
@@ -848,6 +895,7 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
             return;
         }
     }
+    cnt.ev(EV_COMB_GEN);
     // Finite events in push order a0, a1, b0, b1 (csg.cpp:76-81).
     real et[4];
     int ec[4];
@@ -969,6 +1017,11 @@ __device__ __forceinline__ void csg_c(int op, const CIvl& A, const CIvl& B, CIvl
 // result, only skips work no lane needs.
 constexpr float RT_INF_F = __builtin_inff();
 
+// Square root for the f32 cull tests: the hardware v_sqrt_f32 (~1 ulp, one
+// instruction) instead of the correctly rounded sequence (~15): every test
+// carries a margin of >= 1e-6 of the magnitudes involved, far above 1 ulp.
+__device__ __forceinline__ float sqrt_cull(float x) { return __builtin_amdgcn_sqrtf(x); }
+
 struct FRay {
     float ox, oy, oz, dx, dy, dz;
 };
@@ -1074,6 +1127,7 @@ __device__ __forceinline__ CIvl run_compact(const DevScene& S, int pc0, int pc1,
 template <class CT>
 __device__ __forceinline__ void fold_leaf_ivl(const FoldT& L, const DRay& r, CIvl& o, CT& cnt) {
     cnt.inc(RT_OPC_SPHERE_IVL);
+    cnt.ev(EV_FOLD_LEAF);
     o.c0 = L.pc;
     o.c1 = L.pc | REF_ROOT1;
     const real r0 = L.r;
@@ -1429,7 +1483,7 @@ __device__ __forceinline__ bool line_touch(const float* g, float ox, float oy, f
     const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
     if (!(L2 > R * R)) return true;
     const float wa = __builtin_fabsf(__builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az)));
-    const float rhs = cth * __builtin_sqrtf(L2 - R * R) - sth * R;
+    const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
     return !(wa + m < rhs);
 }
 
@@ -1453,6 +1507,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
     const bool fin = __builtin_isfinite(Ax + Ay + Az + Bx + By + Bz);
     const uint64_t nm = __ballot(need);
     if (!nm) return false;
+    cnt.ev(EV_SHQ);
     // without the capsule (a partially active wave, or unbounded / non-finite
     // segments) every object is a candidate and each bounded one gets the
     // per-lane segment test
@@ -1463,7 +1518,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
     float da = (Ax - ax) * (Ax - ax) + (Ay - ay) * (Ay - ay) + (Az - az) * (Az - az);
     float db = (Bx - bx) * (Bx - bx) + (By - by) * (By - by) + (Bz - bz) * (Bz - bz);
     const float d = need ? __builtin_fmaxf(da, db) : 0.0f;
-    const float rho = uni<UO>(cap ? __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(d)))) : 0.0f);
+    const float rho = uni<UO>(cap ? sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(d)))) : 0.0f);
     const float ux = uni<UO>(bx - ax), uy = uni<UO>(by - ay), uz = uni<UO>(bz - az);
     const float uu = uni<UO>(__builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz)));
     const float mag = uni<UO>(__builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
@@ -1515,6 +1570,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            cnt.ev(EV_SH_CAND);
             cnt.pb(PH_OBJ_PREF);
             // CSG objects: no lane's segment reaches a leaf ball (DevObj::pb0);
             // otherwise the leaves whose balls no querying lane's line meets
@@ -1535,10 +1591,10 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
                     const float do2 = need ? dxo * dxo + dyo * dyo + dzo * dzo : 0.0f;
                     const float dc = need ? __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, lax, __builtin_fmaf(fr.dy, lay, fr.dz * laz)))
                                           : 0.0f;
-                    lrho = uni<UO>(__builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(do2)))));
+                    lrho = uni<UO>(sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(do2)))));
                     const float dcm = __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f;
                     lcth = uni<UO>(1.0f - dcm);
-                    lsth = uni<UO>(__builtin_sqrtf(__builtin_fmaxf(0.0f, 1.0f - lcth * lcth)) + 1e-6f);
+                    lsth = uni<UO>(sqrt_cull(__builtin_fmaxf(0.0f, 1.0f - lcth * lcth)) + 1e-6f);
                     lmag = uni<UO>(__builtin_fabsf(lox) + __builtin_fabsf(loy) + __builtin_fabsf(loz) + lrho + 1.0f);
                 }
 #ifdef RT_NO_LEAF_MASK
@@ -1559,6 +1615,8 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             const bool csg_obj = ob.kind == rtamd::OBJ_CHAIN && ob.core != 0;
             if (csg_obj) cnt.pb(PH_SHADOW_CSG);
             cnt.pb(PH_OBJ_HIT);
+            cnt.ev(EV_SH_HIT);
+            if (csg_obj) cnt.ev(EV_SH_CSG);
             if (need && !hit) {
                 real t = RV(0.0), ts = RV(0.0);
                 V3 p;
@@ -1592,7 +1650,7 @@ __device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, f
     if (!(L2 > R * R)) return true;   // the bundle's origin region touches the ball (or NaN)
     const float wa = __builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az));
     // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R
-    const float rhs = cth * __builtin_sqrtf(L2 - R * R) - sth * R;
+    const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
     return !(wa + m < rhs);
 }
 
@@ -1610,11 +1668,11 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     const float do2 = (fr.ox - ox) * (fr.ox - ox) + (fr.oy - oy) * (fr.oy - oy) + (fr.oz - oz) * (fr.oz - oz);
     // 1 - cos(angle to the axis), >= 0 up to rounding
     const float dc = __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, ax, __builtin_fmaf(fr.dy, ay, fr.dz * az)));
-    const float rho = cone ? __builtin_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(do2)))) : 0.0f;
+    const float rho = cone ? sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(do2)))) : 0.0f;
     const float dcm = cone ? __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f : 2.0f;   // rounding of unit dots
     const float cth = 1.0f - dcm;
     const bool wide = !(cth > 0.0f);   // a bundle wider than 90 degrees (or no cone): no culling
-    const float sth = __builtin_sqrtf(__builtin_fmaxf(0.0f, 1.0f - cth * cth)) + 1e-6f;
+    const float sth = sqrt_cull(__builtin_fmaxf(0.0f, 1.0f - cth * cth)) + 1e-6f;
     const float mag = __builtin_fabsf(ox) + __builtin_fabsf(oy) + __builtin_fabsf(oz) + rho + 1.0f;
     const int lane = __lane_id();
     real closest = tmax;
@@ -1647,6 +1705,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             m &= m - 1;
             const DevObj ob = S.objs[o];
             if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            cnt.ev(EV_PR_CAND);
             cnt.pb(PH_OBJ_PREF);
             // CSG objects: the bundle reaches no leaf ball (DevObj::pb0);
             // otherwise the leaves whose balls no lane's line meets
@@ -1683,6 +1742,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             const bool csg_obj = ob.kind == rtamd::OBJ_CHAIN && ob.core != 0;
             if (csg_obj) cnt.pb(PH_PRIMARY_CSG);
             cnt.pb(PH_OBJ_HIT);
+            cnt.ev(EV_PR_HIT);
             if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt, lmask, use_mask)) {
                 closest = t;
                 win = o;
@@ -1737,6 +1797,23 @@ __device__ __forceinline__ double pow_spec(double x, double y) {
     return h + l;
 }
 __device__ __forceinline__ float pow_spec(float x, float y) { return pow(x, y); }
+
+// Per-lane LDS pool of a 256-thread workgroup: shade() keeps pass 1's light
+// geometry (wi, dist) of the first kLightCache lights of each light chunk
+// there for pass 2, instead of recomputing sqrt + three divisions per lit
+// light; flush_counters() reuses the slots of each wave's own lanes at the
+// end.  kLightCache x 4 x 256 doubles = 40 KiB: four workgroups (16 waves)
+// still fit a CU's 160 KiB.  Layout [light][field][thread]: consecutive lanes
+// read consecutive 8-byte words (no bank conflicts).
+#ifndef RT_LIGHT_CACHE
+#define RT_LIGHT_CACHE 5
+#endif
+constexpr int kLightCache = RT_LIGHT_CACHE;
+constexpr int kPoolThreads = 256;
+__device__ __forceinline__ double* lds_pool() {
+    __shared__ double pool[(kLightCache > 0 ? kLightCache : 1) * 4 * kPoolThreads];
+    return pool;
+}
 
 __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
     return v3(RV(1.0) - (RV(1.0) - a.x) * (RV(1.0) - b.x), RV(1.0) - (RV(1.0) - a.y) * (RV(1.0) - b.y), RV(1.0) - (RV(1.0) - a.z) * (RV(1.0) - b.z));
@@ -1799,6 +1876,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
         E = combine(E, combine(Ed, Es));
     }
     if (WV) cnt.pb(PH_SHADE2);   // (pass 2 is timed from the end of pass 1; this start is overwritten)
+    double* const lc = lds_pool() + threadIdx.x;
     for (int l0 = 0; __any(valid) && l0 < S.n_lights; l0 += 32) {
         const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
         uint32_t lit = 0;
@@ -1812,12 +1890,20 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             const real dist = sqrt_r(d2);
             const auto wq = div3(tl.x, tl.y, tl.z, dist);
             const V3 wi = v3(wq.x, wq.y, wq.z);
+            if (li - l0 < kLightCache) {
+                double* c = lc + (li - l0) * 4 * kPoolThreads;
+                c[0] = wi.x;
+                c[kPoolThreads] = wi.y;
+                c[2 * kPoolThreads] = wi.z;
+                c[3 * kPoolThreads] = dist;
+            }
             const real ndotl = dmax(RV(0.0), dot3(n, wi));
             const real max_t = dist - eps;
             // shading.cpp:86-103: back-facing lights and lights closer than
             // the shadow epsilon are skipped before the occlusion query
             const bool need = valid && ndotl > RV(0.0) && max_t > eps;
             if (!__any(need)) continue;
+            cnt.ev(EV_LIGHT1);
             const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
             const DRay sr = make_ray(so, wi);
             bool occ = false;
@@ -1843,13 +1929,22 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
         const V3 alb = ld3(m->albedo);
         for (int li = l0; li < l1; ++li) {
             if (!((lit >> (li - l0)) & 1u)) continue;
+            cnt.ev(EV_LIGHT2);
             const LightT* L = &S.lights[li];
-            V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
-            real d2 = dot3(tl, tl);
-            if (d2 <= RV(0.01)) d2 = RV(0.01);
-            const real dist = sqrt_r(d2);
-            const auto wq = div3(tl.x, tl.y, tl.z, dist);
-            const V3 wi = v3(wq.x, wq.y, wq.z);
+            V3 wi;
+            real dist;
+            if (li - l0 < kLightCache) {   // pass 1's values (same lane)
+                const double* c = lc + (li - l0) * 4 * kPoolThreads;
+                wi = v3((real)c[0], (real)c[kPoolThreads], (real)c[2 * kPoolThreads]);
+                dist = (real)c[3 * kPoolThreads];
+            } else {
+                V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
+                real d2 = dot3(tl, tl);
+                if (d2 <= RV(0.01)) d2 = RV(0.01);
+                dist = sqrt_r(d2);
+                const auto wq = div3(tl.x, tl.y, tl.z, dist);
+                wi = v3(wq.x, wq.y, wq.z);
+            }
             const real ndotl = dmax(RV(0.0), dot3(n, wi));
             cnt.inc(RT_OPC_SHADE_LIGHT);
             const real ed = dmax(RV(0.5), dist);

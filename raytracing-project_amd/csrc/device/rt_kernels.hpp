@@ -40,12 +40,17 @@ constexpr int kStdBlockY = kStdWPB >= 4 ? 4 : 2;            // output rows per w
 
 template <bool C, int NWAVES = 4>
 __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
-#ifdef RT_PHASE_PROF
+#if defined(RT_EVENT_PROF)
+    constexpr int NW = C ? 18 : 2 + EV_COUNT;
+#elif defined(RT_PHASE_PROF)
     constexpr int NW = C ? 18 : 2 + PH_COUNT;
 #else
     constexpr int NW = C ? 18 : 2;
 #endif
-    __shared__ unsigned long long red[NWAVES][NW];
+    // red[w][k] lives in wave w's own lanes' slots of the LDS pool (those
+    // lanes are done with shading when their wave gets here)
+    static_assert(NW <= 64 && NWAVES * 64 <= kPoolThreads, "counter slots");
+    unsigned long long(*red)[64] = reinterpret_cast<unsigned long long(*)[64]>(lds_pool());
     unsigned long long v[NW];
     v[0] = ni;
     v[1] = no;
@@ -53,7 +58,12 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[2 + k] = cnt.c[k];
     }
-#ifdef RT_PHASE_PROF
+#if defined(RT_EVENT_PROF)
+    if constexpr (!C) {
+#pragma unroll
+        for (int k = 0; k < EV_COUNT; ++k) v[2 + k] = (threadIdx.x & 63) == 0 ? cnt.get(k) : 0ull;
+    }
+#elif defined(RT_PHASE_PROF)
     if constexpr (!C) {
 #pragma unroll
         for (int k = 0; k < PH_COUNT; ++k) v[2 + k] = (threadIdx.x & 63) == 0 ? cnt.get(k) : 0ull;
@@ -99,6 +109,7 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     cnt.init();
     V3 c = v3(RV(0.0), RV(0.0), RV(0.0));
     if (active) {
+        cnt.ev(EV_WAVES);
         cnt.pb(PH_SETUP);
         const int r = P.rows[ri];
         const int y = P.H - 1 - r;   // loop row (tracer.cpp:297 writes row ny-1-y)
