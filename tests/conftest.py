@@ -3,6 +3,15 @@ import sys
 
 import pytest
 
+# torch first: its bundled HIP runtime (soname libamdhip64.so.7, like
+# /opt/rocm's) is then the process's one runtime, as in bench.py and the
+# tools.  Loading librtamd.so first and torch later inside a test aborted
+# the process at exit (heap corruption in runtime teardown) on the GPU box.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY = os.path.join(REPO, "raytracing-project_amd", "python")
 if PY not in sys.path:
