@@ -276,6 +276,7 @@ struct DevScene {
     const DevObj* objs;
     const DevOp* ops;
     const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
+    const float4* ctab; // per object 2 x float4: wave-level cull record (CompiledScene::ctab)
     const FoldT* fold;  // fold objects' leaf tables (DevObj::fold0)
     int n_lights, n_objs;
     int n_dlights;
@@ -1457,16 +1458,20 @@ __device__ __forceinline__ float uni(float v) {
 }
 
 
-__device__ __forceinline__ bool capsule_touch(const float* g, float ax, float ay, float az, float ux, float uy,
+__device__ __forceinline__ bool capsule_touch(const float4 g, float ax, float ay, float az, float ux, float uy,
                                               float uz, float uu, float rho, float mag) {
-    const float wx = g[0] - ax, wy = g[1] - ay, wz = g[2] - az;
+    const float wx = g.x - ax, wy = g.y - ay, wz = g.z - az;
     const float wu = __builtin_fmaf(wx, ux, __builtin_fmaf(wy, uy, wz * uz));
     const float s = uu > 0.0f ? __builtin_amdgcn_fmed3f(wu * __builtin_amdgcn_rcpf(uu), 0.0f, 1.0f) : 0.0f;
     const float qx = __builtin_fmaf(-s, ux, wx), qy = __builtin_fmaf(-s, uy, wy), qz = __builtin_fmaf(-s, uz, wz);
     const float d2 = __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz));
-    const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
-    const float R = g[3] + rho + m;
+    const float m = 1e-5f * (mag + __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w);
+    const float R = g.w + rho + m;
     return !(d2 > R * R);   // NaN passes
+}
+__device__ __forceinline__ bool capsule_touch(const float* g, float ax, float ay, float az, float ux, float uy,
+                                              float uz, float uu, float rho, float mag) {
+    return capsule_touch(*reinterpret_cast<const float4*>(g), ax, ay, az, ux, uy, uz, uu, rho, mag);
 }
 
 // The same bundle seen as LINES (Primitive::interval has no range, so a CSG
@@ -1497,6 +1502,9 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
 template <bool EAGER, bool DEEP, bool UO, class CT>
 __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
+#if defined(RT_ABL_SHADOW) && RT_ABL_SHADOW == 1   // diagnostic ablation (wrong images): no shadow queries
+    return false;
+#endif
     cnt.pb(PH_WAVE_SETUP);
     const FRay fr = to_fray(r);
     const float ftmin = (float)tmin, ftmax = (float)tmax;
@@ -1534,20 +1542,22 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         const int j = base + lane;
         bool pass = false;
         if (j < S.n_objs) {
-            const DevObj& ob = S.objs[j];
-            if (ob.kind == rtamd::OBJ_HALF && cap) {
+            // the object's cull record (CompiledScene::ctab): one 32-byte load
+            const float4 c0 = S.ctab[2 * j], c1 = S.ctab[2 * j + 1];
+            const int type = __float_as_int(c1.x);
+            if (!cap) {
+                pass = type != 0;
+            } else if (type == 3) {
                 // a bare half-space: the segments cross its plane only if the
-                // capsule does (both axis ends farther than rho on one side: no lane)
-                const NodeT* nd = &S.nodes[ob.node];
-                const float nx = (float)nd->v[3], ny = (float)nd->v[4], nz = (float)nd->v[5];
-                const float px = (float)nd->v[0], py = (float)nd->v[1], pz = (float)nd->v[2];
-                const float sa = nx * (ax - px) + ny * (ay - py) + nz * (az - pz);
-                const float sb = nx * (bx - px) + ny * (by - py) + nz * (bz - pz);
-                const float m = rho + 1e-5f * (mag + __builtin_fabsf(px) + __builtin_fabsf(py) + __builtin_fabsf(pz));
+                // capsule does (both axis ends farther than rho on one side: no
+                // lane); n.x - n.p in f32 is within 1e-6 of the magnitudes of the
+                // signed distance, far inside the margin
+                const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
+                const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
+                const float m = rho + 1e-5f * (mag + c1.y);
                 pass = !((sa > m && sb > m) || (sa < -m && sb < -m));   // NaN passes
             } else {
-                pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
-                       (!ob.has_bound || !cap || capsule_touch(ob.fb, ax, ay, az, ux, uy, uz, uu, rho, mag));
+                pass = type == 1 || (type == 2 && capsule_touch(c0, ax, ay, az, ux, uy, uz, uu, rho, mag));
             }
         }
         // (lane j tests object j only with the whole wave active; otherwise
@@ -1555,6 +1565,9 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         const int nc = S.n_objs - base;
         uint64_t m = cap ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
+#if defined(RT_ABL_SHADOW) && RT_ABL_SHADOW == 2   // diagnostic: setup + transposed test only
+        if (m != 12345) return false;
+#endif
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             if (need) {
                 int skipped = 0;
@@ -1617,6 +1630,9 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_SH_HIT);
             if (csg_obj) cnt.ev(EV_SH_CSG);
+#if defined(RT_ABL_SHADOW) && RT_ABL_SHADOW == 3   // diagnostic: everything but object_hit
+            if (m != 12345) continue;
+#endif
             if (need && !hit) {
                 real t = RV(0.0), ts = RV(0.0);
                 V3 p;
@@ -1641,17 +1657,21 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
 // over those, in scene order, exactly as scene_intersect (ties and the
 // shrinking closest-so-far included).  Conservative in f32 like
 // capsule_touch: results are unchanged.
-__device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
+__device__ __forceinline__ bool cone_touch(const float4 g, float ox, float oy, float oz, float ax, float ay,
                                           float az, float cth, float sth, float rho, float mag) {
-    const float wx = g[0] - ox, wy = g[1] - oy, wz = g[2] - oz;
-    const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
-    const float R = g[3] + rho + m;
+    const float wx = g.x - ox, wy = g.y - oy, wz = g.z - oz;
+    const float m = 1e-5f * (mag + __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w);
+    const float R = g.w + rho + m;
     const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
     if (!(L2 > R * R)) return true;   // the bundle's origin region touches the ball (or NaN)
     const float wa = __builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az));
     // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R
     const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
     return !(wa + m < rhs);
+}
+__device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
+                                          float az, float cth, float sth, float rho, float mag) {
+    return cone_touch(*reinterpret_cast<const float4*>(g), ox, oy, oz, ax, ay, az, cth, sth, rho, mag);
 }
 
 template <bool EAGER, bool DEEP, class CT>
@@ -1685,9 +1705,9 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
         const int j = base + lane;
         bool pass = false;
         if (j < S.n_objs) {
-            const DevObj& ob = S.objs[j];
-            pass = ob.kind != rtamd::OBJ_GROUP && ob.kind != rtamd::OBJ_NEVER &&
-                   (!ob.has_bound || wide || cone_touch(ob.fb, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+            const float4 c0 = S.ctab[2 * j], c1 = S.ctab[2 * j + 1];
+            const int type = __float_as_int(c1.x);
+            pass = type != 0 && (type != 2 || wide || cone_touch(c0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
         }
         const int nc = S.n_objs - base;
         uint64_t m = cone ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));

@@ -295,6 +295,7 @@ DevScene make_scene(const SceneView& V) {
     S.objs = V.objs;
     S.ops = V.ops;
     S.gb = V.gb;
+    S.ctab = reinterpret_cast<const float4*>(V.ctab);
     S.fold = static_cast<const FoldT*>(V.fold);
     S.n_lights = V.n_lights;
     S.n_dlights = V.n_dlights;

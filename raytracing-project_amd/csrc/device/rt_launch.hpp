@@ -69,6 +69,7 @@ struct SceneView {
     const DevObj* objs;
     const DevOp* ops;
     const float* gb;
+    const float* ctab;   // CompiledScene::ctab
     const void* fold;   // FoldLeafR of the launching precision
     int n_lights, n_dlights, n_objs;
     int n_bounded;

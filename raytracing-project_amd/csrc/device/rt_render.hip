@@ -111,7 +111,7 @@ struct SceneCache {
 // Per-device workspace (one render at a time per device; guarded by a mutex).
 struct Workspace {
     std::mutex mu;
-    DBuf nodes, mats, lights, dlights, objs, ops, gb;
+    DBuf nodes, mats, lights, dlights, objs, ops, gb, ctab;
     DBuf fold;
     DBuf nodes_f, mats_f, lights_f, dlights_f, fold_f;   // float copies (RT_FLAG_FP32)
     DBuf rows, jit, ckpt, jscratch, counters;
@@ -284,6 +284,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(upload(ws.objs, sc.cs.objs, st));
         HIP_TRY(upload(ws.ops, sc.cs.ops, st));
         HIP_TRY(upload(ws.gb, sc.cs.gbounds, st));
+        HIP_TRY(upload(ws.ctab, sc.cs.ctab, st));
         sc.uid = rtamd::scene_uid(s);
         sc.fp32 = fp32;
         sc.valid = true;
@@ -344,6 +345,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.objs = ws.objs.as<rtamd::DevObj>();
     S.ops = ws.ops.as<rtamd::DevOp>();
     S.gb = ws.gb.as<float>();
+    S.ctab = ws.ctab.as<float>();
     S.n_lights = d.n_lights;
     S.n_objs = (int)cs.objs.size();
     S.n_bounded = 0;

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <stdexcept>
 
 namespace rtamd {
@@ -439,6 +440,25 @@ public:
         cs.max_ray_depth = max_r_;
         cs.max_ivl_depth = max_i_;
         cs.objs = insert_groups(cs.objs);
+        cs.ctab.assign(cs.objs.size() * 8, 0.0f);
+        for (size_t j = 0; j < cs.objs.size(); ++j) {
+            const DevObj& o = cs.objs[j];
+            float* c = &cs.ctab[8 * j];
+            int type = 1;
+            if (o.kind == OBJ_GROUP || o.kind == OBJ_NEVER) {
+                type = 0;
+            } else if (o.has_bound) {
+                type = 2;
+                for (int k = 0; k < 4; ++k) c[k] = o.fb[k];
+            } else if (o.kind == OBJ_HALF) {
+                type = 3;
+                const double* v = d_.nodes[o.node].v;   // point v[0..2], unit normal v[3..5]
+                for (int k = 0; k < 3; ++k) c[k] = (float)v[3 + k];
+                c[3] = (float)(v[3] * v[0] + v[4] * v[1] + v[5] * v[2]);
+                c[5] = (float)(std::fabs(v[0]) + std::fabs(v[1]) + std::fabs(v[2]));
+            }
+            std::memcpy(&c[4], &type, sizeof(int));
+        }
         return cs;
     }
 

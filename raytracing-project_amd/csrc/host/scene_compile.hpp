@@ -87,6 +87,12 @@ struct CompiledScene {
     std::vector<DevObj> objs;
     std::vector<DevOp> ops;
     std::vector<FoldLeaf> fold;    // leaves of the fold objects (DevObj::fold0)
+    // Wave-level cull record of every object (8 floats, objs order), read by
+    // lane j for object j in the transposed tests: (c, r) of the f32 bound
+    // ball or, for a bare half-space, (n, n.p) of its plane; then the type
+    // (0 never a candidate: group / never-hit, 1 always, 2 ball, 3 plane)
+    // and, for a plane, |px| + |py| + |pz| (the f32 margin's scale).
+    std::vector<float> ctab;
     std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated;
                                    // then the leaf prefilter balls of CHAIN objects (world frame, see DevObj::pb0)
     int max_ray_depth = 0;   // transform nesting on any path of an eager program (chains need no stack)
