@@ -1533,9 +1533,8 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
                           __builtin_fabsf(by) + __builtin_fabsf(bz) + rho + 1.0f);
     const int lane = __lane_id();
     // line bundle for the CSG leaf masks, built on first use (cap only)
-    const float lox = rdlane_f(fr.ox, f), loy = rdlane_f(fr.oy, f), loz = rdlane_f(fr.oz, f);
-    const float lax = rdlane_f(fr.dx, f), lay = rdlane_f(fr.dy, f), laz = rdlane_f(fr.dz, f);
     bool lb_ready = false;
+    float lox = 0.0f, loy = 0.0f, loz = 0.0f, lax = 0.0f, lay = 0.0f, laz = 0.0f;
     float lrho = 0.0f, lcth = -1.0f, lsth = 1.0f, lmag = 0.0f;
     bool hit = false;
     for (int base = 0; base < S.n_objs; base += 64) {
@@ -1600,6 +1599,8 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
                 if (!lb_ready) {
                     // line bundle of the querying lanes (lane f's line as the axis)
                     lb_ready = true;
+                    lox = rdlane_f(fr.ox, f), loy = rdlane_f(fr.oy, f), loz = rdlane_f(fr.oz, f);
+                    lax = rdlane_f(fr.dx, f), lay = rdlane_f(fr.dy, f), laz = rdlane_f(fr.dz, f);
                     const float dxo = fr.ox - lox, dyo = fr.oy - loy, dzo = fr.oz - loz;
                     const float do2 = need ? dxo * dxo + dyo * dyo + dzo * dzo : 0.0f;
                     const float dc = need ? __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, lax, __builtin_fmaf(fr.dy, lay, fr.dz * laz)))
