@@ -46,6 +46,12 @@ int rt_test_kernel_info(const struct rt_scene* s, int mode, int flags, int32_t* 
  * two to be bit-identical. */
 int rt_test_div3(const double* a_host, const double* b_host, int n, double* div3_host, double* plain_host);
 
+/* Host only: the precomputed mt19937 tree jump polynomials in `path` (the
+ * build's lib/mt19937_tree.polys, read by the jitter generator) against the
+ * same polynomials computed in this process, first `levels` levels.
+ * Returns 0 equal, 1 different, 2 file missing / short / corrupt. */
+int rt_test_mt_poly_file(const char* path, int levels);
+
 /* GPU, one device: the multi-GPU frame path of rt_render_multi /
  * rt_render_dist (partition, row chunks, gather stage layout, placement on
  * the root) with `world` simulated ranks rendered one after another on the

@@ -16,7 +16,11 @@
 // and word 454+t reads new word 227+t, so both come from the same thread's
 // registers; only word 623 needs new word 0 (its +1 neighbour), which
 // thread 169 recomputes.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
 #include <stdint.h>
 
 #include <algorithm>
@@ -471,8 +475,24 @@ hipError_t mt_launch_fill(const JitterTable& T, const std::vector<JRange>& range
     return hipGetLastError();
 }
 
+// The precomputed tree polynomials live next to this library
+// (lib/mt19937_tree.polys, written by the build's bin/mt_polygen).
+static void locate_poly_file() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        Dl_info info{};
+        if (dladdr(reinterpret_cast<void*>(&locate_poly_file), &info) && info.dli_fname) {
+            std::string dir(info.dli_fname);
+            const size_t slash = dir.rfind('/');
+            dir = slash == std::string::npos ? std::string(".") : dir.substr(0, slash);
+            mt_set_poly_file(dir + "/mt19937_tree.polys");
+        }
+    });
+}
+
 hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
     release();
+    locate_poly_file();
     std::vector<uint32_t> polys = mt_tree_polys(K_blocks, levels_needed);
     std::vector<uint16_t> taps;
     off.assign(1, 0);

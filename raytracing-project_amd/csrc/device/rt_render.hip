@@ -696,6 +696,17 @@ extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
     }
 }
 
+extern "C" int rt_test_mt_poly_file(const char* path, int levels) {
+    if (!path || levels <= 0) return RT_ERR_INVALID_ARG;
+    try {
+        std::vector<uint32_t> from_file;
+        if (!rtamd::mt_load_tree_polys(path, rtamd::kTableK, levels, from_file)) return 2;
+        return from_file == rtamd::mt_tree_polys_computed(rtamd::kTableK, levels) ? 0 : 1;
+    } catch (...) {
+        return -1;
+    }
+}
+
 extern "C" int rt_test_jitter_device(int K, int64_t q0, int64_t q1, int64_t first, int64_t count,
                                      double* out_host) {
     if (K < 0 || q0 < 0 || q1 <= q0 || (q0 & 1) || (q1 & 1) || !out_host || first * 2 < q0 || (first + count) * 2 > q1)

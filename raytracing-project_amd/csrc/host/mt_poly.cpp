@@ -1,6 +1,7 @@
 // mt_poly.cpp — see mt_poly.hpp.
 #include "mt_poly.hpp"
 
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -265,13 +266,76 @@ std::vector<uint64_t> from_words32(const uint32_t* w, size_t n64) {
 
 }  // namespace
 
+namespace {
+std::string g_poly_file;   // guarded by g_mu
+
+uint64_t fnv1a(const uint32_t* p, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n * 4; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+}  // namespace
+
+void mt_set_poly_file(const std::string& path) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_poly_file = path;
+}
+
+bool mt_load_tree_polys(const std::string& path, int K_blocks, int levels, std::vector<uint32_t>& out) {
+    if (path.empty() || levels <= 0) return false;
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    char magic[8];
+    uint32_t hdr[4];
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "MTJPOLY1", 8) == 0 &&
+              std::fread(hdr, 4, 4, f) == 4 && (int)hdr[0] == K_blocks && (int)hdr[1] >= levels &&
+              hdr[2] == (uint32_t)kPolyWords32;
+    std::vector<uint32_t> all;
+    if (ok) {
+        all.resize((size_t)hdr[1] * (kMTRadix - 1) * kPolyWords32);
+        uint64_t sum = 0;
+        ok = std::fread(all.data(), 4, all.size(), f) == all.size() && std::fread(&sum, 8, 1, f) == 1 &&
+             sum == fnv1a(all.data(), all.size());
+    }
+    std::fclose(f);
+    if (!ok) return false;
+    out.assign(all.begin(), all.begin() + (size_t)levels * (kMTRadix - 1) * kPolyWords32);
+    return true;
+}
+
+bool mt_save_tree_polys(const std::string& path, int K_blocks, int levels) {
+    const std::vector<uint32_t> p = mt_tree_polys_computed(K_blocks, levels);
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const uint32_t hdr[4] = {(uint32_t)K_blocks, (uint32_t)levels, (uint32_t)kPolyWords32, 0u};
+    const uint64_t sum = fnv1a(p.data(), p.size());
+    bool ok = std::fwrite("MTJPOLY1", 1, 8, f) == 8 && std::fwrite(hdr, 4, 4, f) == 4 &&
+              std::fwrite(p.data(), 4, p.size(), f) == p.size() && std::fwrite(&sum, 8, 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    return ok;
+}
+
 std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels) {
     static std::map<std::pair<int, int>, std::vector<uint32_t>> cache;
+    std::string file;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = cache.find({K_blocks, levels});
         if (it != cache.end()) return it->second;
+        file = g_poly_file;
     }
+    std::vector<uint32_t> out;
+    if (!mt_load_tree_polys(file, K_blocks, levels, out)) out = mt_tree_polys_computed(K_blocks, levels);
+    std::lock_guard<std::mutex> lk(g_mu);
+    cache[{K_blocks, levels}] = out;
+    return out;
+}
+
+std::vector<uint32_t> mt_tree_polys_computed(int K_blocks, int levels) {
     const auto& phi = mt_charpoly();
     static Reducer* R = nullptr;
     {
@@ -292,8 +356,6 @@ std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels) {
         }
         for (int k = 1; k < kMTRadix; k <<= 1) square_mod(base, *R);
     }
-    std::lock_guard<std::mutex> lk(g_mu);
-    cache[{K_blocks, levels}] = out;
     return out;
 }
 

@@ -15,6 +15,7 @@
 #pragma once
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 namespace rtamd {
@@ -42,6 +43,20 @@ std::vector<uint32_t> mt_jump_table(int K_blocks, int levels);
 constexpr int kMTRadixBits = 6;
 constexpr int kMTRadix = 1 << kMTRadixBits;
 std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels);
+
+// The tree polynomials are constants of mt19937: the build writes them once
+// (bin/mt_polygen -> lib/mt19937_tree.polys, next to librtamd.so) and
+// mt_tree_polys() reads the levels it needs from that file instead of
+// computing them (~0.5-2 s of GF(2) arithmetic on the first frame of a
+// process).  File: "MTJPOLY1", u32 K, u32 levels, u32 words per polynomial,
+// u32 0, the polynomials in mt_tree_polys order, u64 FNV-1a of the payload.
+// A missing, short or corrupt file is ignored (the polynomials are computed).
+void mt_set_poly_file(const std::string& path);
+bool mt_save_tree_polys(const std::string& path, int K_blocks, int levels);
+// Reads the first `levels` levels from `path` into out; false if unusable.
+bool mt_load_tree_polys(const std::string& path, int K_blocks, int levels, std::vector<uint32_t>& out);
+// mt_tree_polys computed in this process, ignoring the file (tests).
+std::vector<uint32_t> mt_tree_polys_computed(int K_blocks, int levels);
 
 // x^J mod phi for an arbitrary J (kPolyWords32 words).
 std::vector<uint32_t> mt_jump_poly(uint64_t J);
