@@ -85,7 +85,12 @@ int mt_levels_needed(int K, int64_t q1);
 // checkpoints beyond the table) and kept resident; every frame then
 // regenerates ALL of its jitter draws from it (k_mt_fill_w: one wavefront
 // per kTableK-block segment, no per-frame jumps).
-constexpr int kTableK = 64;
+// 16 twist blocks per segment: the fill's floor is one wave's sequential walk
+// through a segment, so shorter segments cut a rank's jitter time at N > 1
+// (8-rank share of config 4: 0.174 -> 0.086 ms) at 4x the table (66 MB for
+// a 4K frame, built once per device).  bin/mt_polygen writes the tree
+// polynomials for this K (tests/test_mt_poly_file.py keeps the two in step).
+constexpr int kTableK = 16;
 struct JitterTable {
     JitterPlan plan;                  // K = kTableK
     uint32_t* d_table = nullptr;      // [cap][624] windows

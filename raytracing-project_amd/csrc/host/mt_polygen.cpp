@@ -1,7 +1,7 @@
 // mt_polygen.cpp — build tool: writes the mt19937 checkpoint-tree jump
-// polynomials (mt_poly.hpp mt_tree_polys, K = 64 twist blocks per segment)
-// to a file that librtamd.so reads at run time instead of recomputing them.
-// Usage: mt_polygen <out-file> [levels]
+// polynomials (mt_poly.hpp mt_tree_polys, K twist blocks per segment =
+// mt_jump.hpp kTableK) to a file that librtamd.so reads at run time instead
+// of recomputing them.  Usage: mt_polygen <out-file> [levels] [K]
 #include <cstdio>
 #include <cstdlib>
 
@@ -13,8 +13,9 @@ int main(int argc, char** argv) {
         return 2;
     }
     const int levels = argc > 2 ? std::atoi(argv[2]) : 4;
-    if (levels < 1 || levels > 8) return 2;
-    if (!rtamd::mt_save_tree_polys(argv[1], 64, levels)) {
+    const int K = argc > 3 ? std::atoi(argv[3]) : 16;
+    if (levels < 1 || levels > 8 || K < 1) return 2;
+    if (!rtamd::mt_save_tree_polys(argv[1], K, levels)) {
         std::fprintf(stderr, "mt_polygen: cannot write %s\n", argv[1]);
         return 1;
     }
