@@ -144,9 +144,11 @@ struct rt_dist {
     ncclComm_t comm = nullptr;
     bool own_comm = false;
     hipStream_t comm_st = nullptr;            // collectives + placement (high priority)
+    hipStream_t alt_st = nullptr;             // odd trace chunks (a chunk's tail overlaps the next chunk)
     DevBuf mine, mine8, stage, rowtab;
     hipEvent_t ev_chunk[kChunks] = {};
     hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
+    hipEvent_t ev_alt = nullptr;              // end of alt_st's work in a frame (joined into st)
     hipEvent_t ev_tb[2 * kChunks] = {};
     std::vector<int32_t> rowtab_host;          // source of the async row-table upload
     std::mutex mu;                            // one frame at a time per rank
@@ -160,10 +162,12 @@ int dist_init_streams(rt_dist& D) {
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_TRY(hipStreamCreateWithPriority(&D.comm_st, hipStreamNonBlocking, hi));
+    HIP_TRY(hipStreamCreateWithFlags(&D.alt_st, hipStreamNonBlocking));
     for (auto& e : D.ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : D.ev_tb) HIP_TRY(hipEventCreate(&e));
     HIP_TRY(hipEventCreate(&D.ev_g0));
     HIP_TRY(hipEventCreate(&D.ev_g1));
+    HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
     return RT_OK;
 }
 
@@ -214,18 +218,19 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     if (D.world > 1) HIP_TRY(hipEventRecord(D.ev_g0, D.comm_st));
     for (size_t k = 0; k < bounds.size() && rc == RT_OK; ++k) {
         const int a = bounds[k].first, b = bounds[k].second, hi = std::min(b, n);
-        if (hi > a) rc = rt_frame_trace(f, a, hi, fb_rows + (size_t)a * row_elems, st);
+        const hipStream_t cst = (k & 1) ? D.alt_st : st;   // chunks alternate between two streams
+        if (hi > a) rc = rt_frame_trace(f, a, hi, fb_rows + (size_t)a * row_elems, cst);
         if (rc != RT_OK) break;
         if (kind == 1 && hi > a) {
             uint8_t* dst8 = D.world > 1 ? D.mine8.as<uint8_t>() + (size_t)a * row_elems : static_cast<uint8_t*>(out_root);
-            if (hipEventRecord(D.ev_tb[n_tb++], st) != hipSuccess) { rc = RT_ERR_HIP; break; }
-            rc = rt_framebuffer_to_rgb8_device(fb_rows + (size_t)a * row_elems, (size_t)(hi - a) * W, dst8, st);
+            if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) { rc = RT_ERR_HIP; break; }
+            rc = rt_framebuffer_to_rgb8_device(fb_rows + (size_t)a * row_elems, (size_t)(hi - a) * W, dst8, cst);
             if (rc != RT_OK) break;
-            if (hipEventRecord(D.ev_tb[n_tb++], st) != hipSuccess) { rc = RT_ERR_HIP; break; }
+            if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) { rc = RT_ERR_HIP; break; }
         }
         if (D.world == 1) continue;
         // chunk k -> root: ONE collective, ordered after the chunk's trace
-        if (hipEventRecord(D.ev_chunk[k], st) != hipSuccess || hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess) {
+        if (hipEventRecord(D.ev_chunk[k], cst) != hipSuccess || hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess) {
             rtamd::set_last_error("rt_render_dist: event chaining failed");
             rc = RT_ERR_HIP;
             break;
@@ -257,7 +262,11 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         }
     }
     if (D.world > 1) (void)hipEventRecord(D.ev_g1, D.comm_st);
-    const int rc_end = rt_frame_end(f, stats);   // joins and synchronises the trace stream
+    // alt_st's last work (a chunk's toByte) into st, which rt_frame_end synchronises
+    if (hipEventRecord(D.ev_alt, D.alt_st) != hipSuccess || hipStreamWaitEvent(st, D.ev_alt, 0) != hipSuccess) {
+        if (rc == RT_OK) rc = RT_ERR_HIP;
+    }
+    const int rc_end = rt_frame_end(f, stats);   // joins and synchronises the trace streams
     if (D.world > 1 && hipStreamSynchronize(D.comm_st) != hipSuccess && rc == RT_OK) {
         rtamd::set_last_error("rt_render_dist: gather stream failed");
         rc = RT_ERR_HIP;
@@ -464,6 +473,8 @@ extern "C" void rt_dist_destroy(rt_dist* d) {
     for (auto e : d->ev_tb) if (e) (void)hipEventDestroy(e);
     if (d->ev_g0) (void)hipEventDestroy(d->ev_g0);
     if (d->ev_g1) (void)hipEventDestroy(d->ev_g1);
+    if (d->alt_st) (void)hipStreamDestroy(d->alt_st);
+    if (d->ev_alt) (void)hipEventDestroy(d->ev_alt);
     (void)hipSetDevice(prev);
     delete d;
 }
@@ -515,6 +526,8 @@ extern "C" int rt_test_render_dist_sim(const rt_scene* s, int W, int H, int mode
         for (auto e : d->ev_tb) if (e) (void)hipEventDestroy(e);
         if (d->ev_g0) (void)hipEventDestroy(d->ev_g0);
         if (d->ev_g1) (void)hipEventDestroy(d->ev_g1);
+        if (d->alt_st) (void)hipStreamDestroy(d->alt_st);
+        if (d->ev_alt) (void)hipEventDestroy(d->ev_alt);
     }
     stage.release();
     out.release();

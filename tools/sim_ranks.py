@@ -41,7 +41,9 @@ def main():
     ap.add_argument("--strip", type=int, default=frame_dist.STRIP)
     ap.add_argument("--chunks", type=int, default=4, help="trace through rt_frame_* in this many chunks")
     ap.add_argument("--rgb8", action="store_true", help="gather 3 B/px (the CLI path) instead of FP64")
-    ap.add_argument("--two-streams", action="store_true", help="alternate chunks between two streams")
+    ap.add_argument("--one-stream", dest="two_streams", action="store_false",
+                    help="all chunks on one stream (the product alternates two, rt_dist.hip)")
+    ap.set_defaults(two_streams=True)
     args = ap.parse_args()
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
