@@ -194,7 +194,7 @@ enum RtEvent {
     EV_COMB_GEN,       //   general sweep
     EV_LIGHT1,         // light pass 1 iterations with some lane needing a query
     EV_LIGHT2,         // light pass 2 iterations (lit lights)
-    EV_DIV3_SLOW,      // div3 one-by-one fallback
+    EV_UNUSED13,       // (free slot)
     EV_COMPACT_LEAF,   // leaf_ivl_c executions
     EV_WAVES,          // waves with an active lane
     EV_COUNT
@@ -1502,9 +1502,6 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
 template <bool EAGER, bool DEEP, bool UO, class CT>
 __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
-#if defined(RT_ABL_SHADOW) && RT_ABL_SHADOW == 1   // diagnostic ablation (wrong images): no shadow queries
-    return false;
-#endif
     cnt.pb(PH_WAVE_SETUP);
     const FRay fr = to_fray(r);
     const float ftmin = (float)tmin, ftmax = (float)tmax;
@@ -1564,9 +1561,6 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         const int nc = S.n_objs - base;
         uint64_t m = cap ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
-#if defined(RT_ABL_SHADOW) && RT_ABL_SHADOW == 2   // diagnostic: setup + transposed test only
-        if (m != 12345) return false;
-#endif
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             if (need) {
                 int skipped = 0;
@@ -1631,9 +1625,6 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_SH_HIT);
             if (csg_obj) cnt.ev(EV_SH_CSG);
-#if defined(RT_ABL_SHADOW) && RT_ABL_SHADOW == 3   // diagnostic: everything but object_hit
-            if (m != 12345) continue;
-#endif
             if (need && !hit) {
                 real t = RV(0.0), ts = RV(0.0);
                 V3 p;

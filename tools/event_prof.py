@@ -19,7 +19,7 @@ import scenes  # noqa: E402
 
 EVENTS = ["shadow_queries", "shadow_candidates", "shadow_object_hits", "shadow_csg_hits", "primary_candidates",
           "primary_object_hits", "fold_leaves", "csg_combines", "comb_single", "comb_union_easy", "comb_general",
-          "light_pass1", "light_pass2", "div3_slow", "compact_leaves", "waves"]
+          "light_pass1", "light_pass2", "(unused)", "compact_leaves", "waves"]
 
 
 def main():
