@@ -305,6 +305,10 @@ def main() -> int:
     if lib.rt_test_kernel_info(sc.handle, mode, flags, ki) == 0:
         occupancy = {"vgprs": ki[0], "scratch_bytes_per_lane": ki[1], "lds_bytes": ki[2],
                      "workgroups_per_cu": ki[3], "waves_per_simd": ki[4], "max_waves_per_simd": 8}
+    kname = C.create_string_buffer(160)
+    kernel_name = "k_std" if mode == 0 else "k_paper_primary"
+    if hasattr(lib, "rt_test_kernel_name") and lib.rt_test_kernel_name(sc.handle, mode, flags, kname, 160) == 0:
+        kernel_name = kname.value.decode()   # as rocprofv3 names it (profiles/*kernel_stats.csv)
 
     # HBM: algorithmic bytes of the trace kernel per launch vs counter-measured traffic.
     px = n_rows * W
@@ -369,7 +373,7 @@ def main() -> int:
                    "cull": not args.no_cull},
         "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),
-                     "traffic": traffic_bytes, "kernel": "k_std" if mode == 0 else "k_paper_primary",
+                     "traffic": traffic_bytes, "kernel": kernel_name,
                      "kernel_ms": round(k_ms, 3), "flops_per_launch": flops / world, "transcendentals": transc,
                      "flops_model": "SURVEY.md 8d table x the reference's own primitive calls (GPU counters, "
                                     "culling off; equal to the CPU oracle's by test)",

@@ -40,6 +40,10 @@ int rt_test_compile_info(const struct rt_scene* s, int32_t* out);
  * culling variant, reflection/refraction variant}.  Needs a device. */
 int rt_test_kernel_info(const struct rt_scene* s, int mode, int flags, int32_t* out);
 
+/* The name of that kernel as rocprofv3 reports it (e.g. "rtd::k_std_lean<false, true>"),
+ * NUL-terminated into out[0 .. cap).  Host only. */
+int rt_test_kernel_name(const struct rt_scene* s, int mode, int flags, char* out, int cap);
+
 /* GPU: the shared-denominator division of the device code (rt_device.hpp
  * div3) next to the compiler's own division on the same inputs:
  * div3_host[3i+k] and plain_host[3i+k] = a[3i+k] / b[i].  Tests require the

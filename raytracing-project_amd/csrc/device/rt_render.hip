@@ -11,6 +11,8 @@
 //   k_paper_finish: edge strength from the stored neighbour hits + hatch.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -747,6 +749,49 @@ extern "C" int rt_test_jitter_device(int K, int64_t q0, int64_t q1, int64_t firs
     (void)hipFree(dj.p);
     (void)hipFree(ds.p);
     return RT_OK;
+}
+
+extern "C" int rt_test_kernel_name(const rt_scene* s, int mode, int flags, char* out, int cap) {
+    if (!s || !out || cap <= 0) return RT_ERR_INVALID_ARG;
+    try {
+        const rt_scene_desc& d = *rt_scene_get_desc(s);
+        const rtamd::CompiledScene cs = rtamd::compile_scene(d);
+        bool secondary = false;
+        for (int i = 0; i < d.n_materials; ++i)
+            if (d.materials[i].kr > 0.0 || d.materials[i].kt > 0.0) secondary = true;
+        if (d.recursion_limit < 2) secondary = false;
+        const bool eager = cs.has_eager;
+        const bool deep = eager || cs.max_ivl_depth > 2 || d.n_dir_lights > 0;
+        int n_bounded = 0;
+        for (const auto& o : cs.objs)
+            if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
+        const bool f32 = (flags & RT_FLAG_FP32) != 0;
+        const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
+        const bool cnt = (flags & RT_FLAG_COUNT_OPS) != 0;
+        const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
+        const bool big = !f32 && (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2 ||
+                                  frames > kMaxDepth);
+        const char* ns = big ? "rtdb" : f32 ? "rtf" : "rtd";
+        auto tf = [](bool b) { return b ? "true" : "false"; };
+        std::string name;
+        if (mode == RT_MODE_PAPER) {
+            if (!big && !eager && !deep)
+                name = std::string("k_paper_primary_lean<") + tf(cnt) + ", " + tf(wv) + ">";
+            else
+                name = std::string("k_paper_primary<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(cnt) + ">";
+        } else if (!big && !eager && !deep && !secondary) {
+            name = std::string("k_std_lean<") + tf(cnt) + ", " + tf(wv) + ">";
+        } else {
+            const bool w = !big && !eager && !deep && wv;   // the WV general variant exists for sec only
+            name = std::string("k_std<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(secondary) + ", " +
+                   tf(cnt) + ", " + tf(w) + ">";
+        }
+        std::snprintf(out, (size_t)cap, "%s::%s", ns, name.c_str());
+        return RT_OK;
+    } catch (const std::exception& e) {
+        rtamd::set_last_error(std::string("scene compile: ") + e.what());
+        return RT_ERR_INVALID_ARG;
+    }
 }
 
 extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32_t* out) {
