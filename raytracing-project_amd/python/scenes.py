@@ -369,3 +369,72 @@ def dir_light_cases(dpi: int = 16) -> dict[str, tuple[str, list]]:
         "reflect_refract_sun": (json.dumps(tort["reflect_refract"]), [sun, back]),
         "pokeball_csg_sun": (json.dumps(tort["pokeball_csg"]), [sun]),
     }
+
+
+def crowd_scene(seed: int, n_objects: int = 150, dpi: int = 16) -> dict:
+    """A seeded random scene with more top-level objects than one wave's
+    transposed cull test covers (64 per pass): spheres (some reflective or
+    refractive), pokeballs, n-ary and binary CSG of spheres (with a half-space
+    now and then), transforms over spheres and CSG, bare half-spaces; 4 point
+    lights, recursion 3.  Exercises the multi-pass wave culling, groups and
+    the fold / compact / eager CSG paths together (tests/test_gpu_crowd.py)."""
+    import random
+    rnd = random.Random(seed)
+
+    def col():
+        m = _mat([rnd.random(), rnd.random(), rnd.random()], shininess=rnd.choice([4, 8, 16, 32]))
+        u = rnd.random()
+        if u < 0.12:
+            m["reflected"] = [0.5, 0.5, 0.5]
+        elif u < 0.2:
+            m["refracted"] = [0.6, 0.6, 0.6]
+        return m
+
+    def pos(spread=3.0):
+        return [rnd.uniform(-spread, spread), rnd.uniform(-1.0, 1.8), rnd.uniform(-7.0, -0.5)]
+
+    def sphere(p=None, r=None):
+        return {"sphere": {"position": p or pos(), "radius": r or rnd.uniform(0.08, 0.45), "color": col(),
+                           "index": rnd.choice([1.0, 1.33, 1.5])}}
+
+    def csg():
+        c = pos()
+        leaves = [sphere([c[0] + rnd.uniform(-0.3, 0.3), c[1] + rnd.uniform(-0.3, 0.3), c[2] + rnd.uniform(-0.3, 0.3)],
+                         rnd.uniform(0.1, 0.4)) for _ in range(rnd.randint(2, 6))]
+        op = rnd.choice(["union", "union", "difference", "intersection"])
+        if op != "union" and rnd.random() < 0.3:
+            # (a half-space only where the CSG stays bounded: a union with one
+            # would contain the camera and reduce every pixel to the
+            # origin-inside entry)
+            leaves.append({"halfSpace": {"position": c, "normal": [rnd.uniform(-1, 1), 1.0, rnd.uniform(-1, 1)],
+                                         "color": col()}})
+        if rnd.random() < 0.3 and len(leaves) >= 2:
+            return {"csg": {"operator": op, "left": leaves[0], "right": {"union": leaves[1:]} if len(leaves) > 2
+                            else leaves[1]}}
+        return {op: leaves}
+
+    def xform(sub):
+        k = rnd.randint(0, 2)
+        if k == 0:
+            return {"translation": {"factors": [rnd.uniform(-0.5, 0.5) for _ in range(3)], "subject": sub}}
+        if k == 1:
+            return {"rotation": {"angle": rnd.uniform(-60, 60), "direction": rnd.randint(0, 2), "subject": sub}}
+        return {"scaling": {"factors": [rnd.uniform(0.6, 1.4) for _ in range(3)], "subject": sub}}
+
+    objs = [{"halfSpace": {"position": [0, -1.3, 0], "normal": [0, 1, 0], "color": col()}}]
+    while len(objs) < n_objects:
+        u = rnd.random()
+        if u < 0.5:
+            objs.append(sphere())
+        elif u < 0.58:
+            objs.append({"pokeball": {"position": pos(), "radius": rnd.uniform(0.15, 0.4),
+                                      "button_dir": [rnd.uniform(-1, 1), rnd.uniform(-1, 1), 1.0]}})
+        elif u < 0.8:
+            objs.append(csg())
+        elif u < 0.97:
+            objs.append(xform(rnd.choice([sphere(), csg()])))
+        else:
+            objs.append({"halfSpace": {"position": [0, 0, -9], "normal": [rnd.uniform(-0.2, 0.2), 0, 1], "color": col()}})
+    lights = [{"position": [rnd.uniform(-6, 6), rnd.uniform(3, 7), rnd.uniform(-2, 6)],
+               "intensity": [rnd.uniform(8, 25)] * 3} for _ in range(4)]
+    return _base(objs, recursion=3, dpi=dpi, lights=lights)

@@ -18,8 +18,10 @@ turned into IR by our loader (librt_host.so).  Outputs are data only:
   deep.npz     frames + counts of the scenes beyond the device's common
                stacks (scenes.deep_scenes: recursion 24, 12 nested
                transforms, a 12-leaf right-nested csg), both modes
+  crowd.npz    frames + counts of the seeded 150-object random scenes
+               (scenes.crowd_scene, seeds 1-3), both modes
 
-Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights deep]
+Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights deep crowd]
 """
 from __future__ import annotations
 
@@ -202,6 +204,23 @@ def make_dirlights():
     print("dirlights:", len(data))
 
 
+CROWD_SEEDS = (1, 2, 3)
+
+
+def make_crowd():
+    """Seeded 150-object random scenes (scenes.crowd_scene), both modes."""
+    data = {}
+    for seed in CROWD_SEEDS:
+        sc = rtamd.load_scene_from_json_text(json.dumps(scenes.crowd_scene(seed)))
+        for mode in (0, 1):
+            with quiet_stdout():
+                fb, ni, no = rtamd.ref_render(sc, sc.width, sc.height, mode)
+            data[f"{seed}/{mode}/fb"] = fb
+            data[f"{seed}/{mode}/counts"] = np.array([ni, no], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "crowd.npz"), **data)
+    print("crowd:", len(data))
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for what in sys.argv[1:]:
@@ -213,3 +232,4 @@ if __name__ == "__main__":
     make_cameras()
     make_dirlights()
     make_deep()
+    make_crowd()
