@@ -72,3 +72,17 @@ def test_crowd_no_cull_same_image(gpu, seed):
     a = gpu.Tracer(sc, W, H, 0).render(gpu.Stats())
     b = gpu.Tracer(sc, W, H, 0, flags=gpu.RT_FLAG_NO_CULL).render(gpu.Stats())
     assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [4, 5])
+def test_crowd_midres_matches_oracle(gpu, seed):
+    """320x240 (more waves per object, so more partial culls) against the
+    oracle at run time (no fixture: the oracle is pinned above)."""
+    sc = gpu.load_scene_from_json_text(json.dumps(scenes.crowd_scene(seed, dpi=80)))
+    W, H = sc.width, sc.height
+    st = gpu.Stats()
+    fb = gpu.Tracer(sc, W, H, 0).render(st)
+    ref, ost = gpu.oracle_render(sc, W, H, 0, threads=16)
+    assert (st.rays_intersect, st.rays_occluded) == (ost.rays_intersect, ost.rays_occluded)
+    assert float(np.abs(fb - ref).max()) <= TOL
