@@ -1409,7 +1409,15 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
             }
         }
         if (ob.kind == rtamd::OBJ_GROUP) continue;
-        if (!hit) {
+        if constexpr (std::is_same<CT, Cnt<false>>::value) {
+            // (every lane evaluates; no divergent region between the loop's
+            // wave-wide tests: see scene_occluded_wave)
+            real t = RV(0.0), ts = RV(0.0);
+            V3 p;
+            int code = 0;
+            const bool h = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
+            hit = hit || h;
+        } else if (!hit) {   // op-counting builds count only the reference's calls
             real t = RV(0.0), ts = RV(0.0);
             V3 p;
             int code = 0;
@@ -1625,7 +1633,20 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_SH_HIT);
             if (csg_obj) cnt.ev(EV_SH_CSG);
-            if (need && !hit) {
+            if constexpr (std::is_same<CT, Cnt<false>>::value) {
+                // every lane evaluates (the wave runs the object anyway) and
+                // only querying lanes without a hit take the result: no
+                // divergent region between this loop's wave-wide tests (the
+                // lane-j-tests-object-j ballots need every lane active; with
+                // `if (need && !hit)` here, the backend's uniform-region
+                // structurization left the exec mask reduced for them and
+                // changed culled shadow decisions)
+                real t = RV(0.0), ts = RV(0.0);
+                V3 p;
+                int code = 0;
+                const bool h = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt, lmask, use_mask);
+                hit = hit || (need && h);
+            } else if (need && !hit) {   // op-counting builds count only the reference's calls
                 real t = RV(0.0), ts = RV(0.0);
                 V3 p;
                 int code = 0;

@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
-L=$PWD/raytracing-project_amd/lib/exp/librtamd_skipu.so
+L=$PWD/raytracing-project_amd/lib/exp/librtamd_${1:-skipu}.so
 timeout -k 10 120 python tools/probe/render_npy.py snorlax 0 gpurun_out/cur.npy 2>&1 | grep -v amdgpu || exit 1
 RTAMD_LIB=$L timeout -k 10 120 python tools/probe/render_npy.py snorlax 0 gpurun_out/skipu.npy 2>&1 | grep -v amdgpu || exit 1
 RTAMD_LIB=$L timeout -k 10 120 python tools/probe/render_npy.py snorlax 0 gpurun_out/skipu_nocull.npy 2 2>&1 | grep -v amdgpu || exit 1
