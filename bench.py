@@ -7,9 +7,14 @@ A "ray" is one Scene::intersect or Scene::occluded query of the reference
 (raytracer/src/scene.cpp:10,33).  A "step" renders one whole frame through the
 product path rt_render_dist (include/rt.h): jitter stream (mt19937 jump-ahead)
 + trace kernels, with the scene resident on the device and the frame left in
-HBM on rank 0.  For N > 1 (one process per GPU, torch.distributed.run) every
-rank renders interleaved 8-row strips of the SAME frame (strong scaling) and
-rank 0 receives them through RCCL ncclGather over xGMI inside librtamd.
+HBM on rank 0.  For N > 1 (one process per GPU, launched by
+torch.distributed.run) every rank renders interleaved 8-row strips of the SAME
+frame (strong scaling) and rank 0 receives them through RCCL ncclGather over
+xGMI inside librtamd.  The process never imports torch: device buffers,
+streams, the max-over-ranks timing and the barriers come from librtamd.so
+(rt_device_alloc, rt_stream_create, rt_dist_reduce_max / rt_dist_barrier over
+RCCL), so the bench runs on /opt/rocm's HIP runtime like the `ray` CLI; the
+RCCL id reaches the other ranks through rendezvous.py.
 
 After the timed region (never inside it): op-counted passes for the FLOP
 model, the wall-clock split of the CLI's end-to-end path (render + device
@@ -113,27 +118,22 @@ def main() -> int:
     ap.add_argument("--fp32-steps", type=int, default=20, help="frames of the FP32 side leg (0 = skip)")
     args = ap.parse_args()
 
-    import numpy as np
-    import torch
+    import numpy as np  # noqa: F401
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=dev)
-
+    import rendezvous
     import rtamd
     import scenes
+
+    # No torch here: librtamd.so brings its own HIP runtime (/opt/rocm's, the
+    # one `ray` uses) and does the collectives over RCCL itself; a second,
+    # torch-bundled runtime in the same process is refused (rtamd.amd_lib).
+    rank, world, local = rendezvous.env_ranks()
+    lib = rtamd.amd_lib()
+    rtamd.set_device(local)
 
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
-    lib = rtamd.amd_lib()
     flags = rtamd.RT_FLAG_NO_CULL if args.no_cull else rtamd.RT_FLAG_NONE
     if args.fp32:
         flags |= rtamd.RT_FLAG_FP32
@@ -142,22 +142,41 @@ def main() -> int:
     uid = (C.c_uint8 * 128)()
     if rank == 0 and lib.rt_dist_get_id(uid) != 0:
         raise RuntimeError(rtamd.last_error())
-    if dist:
-        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
-        dist.broadcast(t, src=0)
-        uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+    if world > 1:
+        got = rendezvous.share_bytes(rank, bytes(uid) if rank == 0 else None, 128)
+        uid = (C.c_uint8 * 128)(*got)
     dh = C.c_void_p()
     if lib.rt_dist_create(uid, world, rank, C.byref(dh)) != 0:
         raise RuntimeError(f"rt_dist_create failed: {rtamd.last_error()}")
+    if world > 1:
+        lib.rt_dist_barrier(dh)   # every rank holds the communicator: the id file can go
+        rendezvous.cleanup(rank)
+
+    def reduce_max(vals):
+        v = (C.c_double * len(vals))(*[float(x) for x in vals])
+        if lib.rt_dist_reduce_max(dh, v, len(vals)) != 0:
+            raise RuntimeError(f"rt_dist_reduce_max failed: {rtamd.last_error()}")
+        return list(v)
+
+    def reduce_sum(vals):   # per-rank slots, max-reduced, summed on the host
+        slots = [0.0] * (len(vals) * world)
+        for i, x in enumerate(vals):
+            slots[i * world + rank] = float(x)
+        m = reduce_max(slots)
+        return [sum(m[i * world:(i + 1) * world]) for i in range(len(vals))]
+
+    def barrier():
+        if lib.rt_dist_barrier(dh) != 0:
+            raise RuntimeError(f"rt_dist_barrier failed: {rtamd.last_error()}")
+
     n_rows = len(rtamd.dist_rows(H, world, rank))
-    frame = torch.zeros((H, W, 3), dtype=torch.float64, device=dev) if rank == 0 else None
-    frame_ptr = C.c_void_p(frame.data_ptr()) if frame is not None else None
-    stream = torch.cuda.current_stream(dev)
+    frame = rtamd.DeviceBuffer(H * W * 3 * 8) if rank == 0 else None
+    frame_ptr = frame.ptr if frame is not None else None
+    stream = rtamd.Stream()
     st = rtamd.Stats()
 
     def step(f=flags, stats=st):
-        rc = lib.rt_render_dist(dh, sc.handle, W, H, mode, f, frame_ptr, C.c_void_p(stream.cuda_stream),
-                                C.byref(stats))
+        rc = lib.rt_render_dist(dh, sc.handle, W, H, mode, f, frame_ptr, stream.handle, C.byref(stats))
         if rc != 0:
             raise RuntimeError(f"rt_render_dist failed ({rc}): {rtamd.last_error()}")
 
@@ -166,10 +185,9 @@ def main() -> int:
     first_ms = (time.perf_counter() - t_first) * 1e3
     for _ in range(max(0, args.warmup - 1)):
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    rtamd.device_synchronize()
+    barrier()
+    rtamd.device_synchronize()
     kernel_ms, rng_ms, gather_ms, rays_local, traced_local = [], [], [], 0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -179,19 +197,14 @@ def main() -> int:
         gather_ms.append(st.ms_gather)
         rays_local += st.rays_intersect + st.rays_occluded
         traced_local += st.rays_traced
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    rtamd.device_synchronize()
+    barrier()
+    rtamd.device_synchronize()
     elapsed = time.perf_counter() - t0
     k_ms = sum(kernel_ms) / len(kernel_ms)
-    if dist:
-        t = torch.tensor([elapsed, k_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, k_ms_max = float(t[0].item()), float(t[1].item())
-        r = torch.tensor([rays_local, traced_local], dtype=torch.float64, device=dev)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        rays_total, traced_total = float(r[0].item()), float(r[1].item())
+    if world > 1:
+        elapsed, k_ms_max = reduce_max([elapsed, k_ms])
+        rays_total, traced_total = reduce_sum([rays_local, traced_local])
     else:
         k_ms_max, rays_total, traced_total = k_ms, float(rays_local), float(traced_local)
 
@@ -203,17 +216,15 @@ def main() -> int:
         s = rtamd.Stats()
         step(f, s)
         v = [int(s.ops[i]) for i in range(16)] + [int(s.rays_occluded)]
-        if dist:
-            tv = torch.tensor(v, dtype=torch.float64, device=dev)
-            dist.all_reduce(tv, op=dist.ReduceOp.SUM)
-            v = [int(x) for x in tv.cpu().tolist()]
+        if world > 1:
+            v = [int(x) for x in reduce_sum(v)]
         d = {rtamd.OP_NAMES[i]: v[i] for i in range(16)}
         d["_occluded"] = v[16]
         return d
 
     ops_ref = counted_pass(flags | rtamd.RT_FLAG_COUNT_OPS | rtamd.RT_FLAG_NO_CULL)
     ops_exe = counted_pass(flags | rtamd.RT_FLAG_COUNT_OPS)
-    torch.cuda.synchronize()
+    rtamd.device_synchronize()
 
     # Side leg (outside the timed region, not the headline): the NON-PARITY
     # FP32 fast path (RT_FLAG_FP32) on the same frame.
@@ -222,37 +233,35 @@ def main() -> int:
         st32 = rtamd.Stats()
         f32 = flags | rtamd.RT_FLAG_FP32
         step(f32, st32)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
+        rtamd.device_synchronize()
+        barrier()
         t32 = time.perf_counter()
         rays32, k32 = 0, []
         for _ in range(args.fp32_steps):
             step(f32, st32)
             rays32 += st32.rays_intersect + st32.rays_occluded
             k32.append(st32.ms_kernel)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
+        rtamd.device_synchronize()
+        barrier()
         e32 = time.perf_counter() - t32
-        if dist:
-            t = torch.tensor([e32], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            e32 = float(t[0].item())
-            r = torch.tensor([rays32], dtype=torch.float64, device=dev)
-            dist.all_reduce(r, op=dist.ReduceOp.SUM)
-            rays32 = float(r.item())
+        if world > 1:
+            e32 = reduce_max([e32])[0]
+            rays32 = reduce_sum([rays32])[0]
         fp32 = {"value": round(rays32 / e32 / 1e6, 3), "unit": "Mrays/s",
                 "ms_per_step": round(e32 / args.fp32_steps * 1e3, 3),
                 "kernel_ms": round(sum(k32) / len(k32), 3), "steps": args.fp32_steps,
                 "note": "RT_FLAG_FP32: non-parity fast path, not within the 1e-5 tolerance (tests/test_gpu_fp32.py)"}
 
-    if rank != 0:
-        if dist:
-            dist.barrier()
+    def teardown():
+        stream.destroy()
+        if frame is not None:
+            frame.free()
         lib.rt_dist_destroy(dh)
-        if dist:
-            dist.destroy_process_group()
+        rtamd.shutdown()
+
+    if rank != 0:
+        barrier()
+        teardown()
         return 0
 
     primary = H * W * (1 if mode == 1 else 8)
@@ -386,10 +395,8 @@ def main() -> int:
         "fp32_fast_path": fp32,
     }
     print(json.dumps(out), flush=True)
-    lib.rt_dist_destroy(dh)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    barrier()
+    teardown()
     return 0
 
 

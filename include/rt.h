@@ -45,10 +45,12 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3   /* 2: rt_scene_desc gained directional lights
+#define RT_ABI_VERSION 4   /* 2: rt_scene_desc gained directional lights
                               3: rt_stats gained the output-path timings; multi-GPU
                                  and device-output entry points (rt_render_multi,
-                                 rt_render_rgb8, rt_dist_*) */
+                                 rt_render_rgb8, rt_dist_*)
+                              4: rt_shutdown, device-buffer utilities, rt_dist_reduce_max /
+                                 rt_dist_barrier */
 
 /* ---------------------------------------------------------------- errors */
 enum rt_status {
@@ -270,6 +272,13 @@ int rt_render_dist(rt_dist* d, const rt_scene* s, int W, int H, int mode, int fl
                    void* hip_stream, rt_stats* stats);
 int rt_render_dist_rgb8(rt_dist* d, const rt_scene* s, int W, int H, int mode, int flags, uint8_t* rgb8_root_dev,
                         void* hip_stream, rt_stats* stats);
+/* Max-reduction of n doubles over all ranks of d, in place on the host
+ * (ncclAllReduce on the rank's collective stream; world 1 without a
+ * communicator: unchanged), and a barrier built on it.  Launcher plumbing
+ * for callers without a collective layer of their own (bench.py's max-over-
+ * ranks timing). */
+int rt_dist_reduce_max(rt_dist* d, double* vals_host, int n);
+int rt_dist_barrier(rt_dist* d);
 /* The partition: writes the output rows of `rank` (ascending) to rows_out
  * (room for H entries) and returns their count; <0 on bad arguments. */
 int rt_dist_rows(int H, int world, int rank, int32_t* rows_out);
@@ -319,6 +328,25 @@ int rt_write_png(const char* path, const uint8_t* rgb8, int W, int H, int n_thre
 
 /* Number of HIP devices visible (0 when none / driver not loaded). */
 int rt_device_count(void);
+
+/* ------------------------------------------ device buffers and teardown
+ * For callers with no device-memory layer of their own (a cgo / JNI / ctypes
+ * binding, tests, bench.py): plain HIP allocations and copies on the
+ * library's own HIP runtime, so a process needs no second one.  All return
+ * an rt_status; sizes are bytes. */
+int rt_set_device(int device);                       /* hipSetDevice for this thread        */
+int rt_device_alloc(size_t bytes, void** dev_out);   /* hipMalloc, zero-filled              */
+int rt_device_free(void* dev);
+int rt_memcpy_h2d(void* dev, const void* host, size_t bytes);
+int rt_memcpy_d2h(void* host, const void* dev, size_t bytes);
+int rt_device_synchronize(void);
+int rt_stream_create(void** stream_out);             /* non-blocking HIP stream              */
+int rt_stream_destroy(void* stream);
+/* Release every device resource the library caches (per-device workspaces,
+ * resident scenes and jitter tables, the rt_render_multi device groups with
+ * their RCCL communicators).  No render may be in flight; later calls
+ * re-create what they need.  The `ray` CLI calls it before exit. */
+int rt_shutdown(void);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,13 @@ int rt_test_mt_poly_file(const char* path, int levels);
 int rt_test_render_dist_sim(const struct rt_scene* s, int W, int H, int mode, int flags, int world, int rgb8,
                             double* fb_host, uint8_t* rgb8_host);
 
+/* GPU, one device: a world-1 rt_dist WITH a real RCCL communicator
+ * (ncclCommInitRank over one rank) whose rt_render_dist frames take the
+ * multi-GPU collective path (row chunks, ncclGather to root 0, placement).
+ * Free with rt_dist_destroy. */
+struct rt_dist;
+int rt_test_dist_create_rccl1(struct rt_dist** out);
+
 #ifdef __cplusplus
 }
 #endif

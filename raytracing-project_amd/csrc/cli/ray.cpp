@@ -72,6 +72,11 @@ int main(int argc, char** argv) {
     if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";
     std::vector<uint8_t> rgb;
+    // device resources (workspaces, RCCL communicators of --gpus N) are
+    // released before exit on every path from here on
+    struct DeviceTeardown {
+        ~DeviceTeardown() { (void)rt_shutdown(); }
+    } teardown;
     const auto t0 = std::chrono::steady_clock::now();
     try {
         tracer.render_rgb8(rgb);

@@ -204,6 +204,7 @@ struct Cnt;
 template <>
 struct Cnt<false> {
     __device__ __forceinline__ void inc(int) {}
+    __device__ __forceinline__ void gate(bool) {}
 #ifdef RT_EVENT_PROF
     __device__ static unsigned long long* acc() {
         __shared__ unsigned long long a[4][EV_COUNT];
@@ -257,11 +258,13 @@ struct Cnt<false> {
 template <>
 struct Cnt<true> {
     uint32_t c[16];
-    __device__ __forceinline__ Cnt() {
+    uint32_t on;   // 0 while a lane evaluates an object only to keep the wave convergent
+    __device__ __forceinline__ Cnt() : on(1u) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = 0;
     }
-    __device__ __forceinline__ void inc(int k) { c[k]++; }
+    __device__ __forceinline__ void inc(int k) { c[k] += on; }
+    __device__ __forceinline__ void gate(bool b) { on = b ? 1u : 0u; }
     __device__ __forceinline__ void ev(int) {}
     __device__ __forceinline__ void init() {}
     __device__ __forceinline__ void pb(int) {}
@@ -1409,20 +1412,17 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
             }
         }
         if (ob.kind == rtamd::OBJ_GROUP) continue;
-        if constexpr (std::is_same<CT, Cnt<false>>::value) {
-            // (every lane evaluates; no divergent region between the loop's
-            // wave-wide tests: see scene_occluded_wave)
-            real t = RV(0.0), ts = RV(0.0);
-            V3 p;
-            int code = 0;
-            const bool h = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
-            hit = hit || h;
-        } else if (!hit) {   // op-counting builds count only the reference's calls
-            real t = RV(0.0), ts = RV(0.0);
-            V3 p;
-            int code = 0;
-            hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
-        }
+        // every lane evaluates (no divergent region between the loop's
+        // wave-wide tests, see scene_occluded_wave); op-counting builds take
+        // the same path and count only the reference's calls (lanes without
+        // a hit yet)
+        real t = RV(0.0), ts = RV(0.0);
+        V3 p;
+        int code = 0;
+        cnt.gate(!hit);
+        const bool h = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt);
+        cnt.gate(true);
+        hit = hit || h;
     }
     return hit;
 }
@@ -1440,6 +1440,15 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
 // ballot gives the objects any lane can reach.  Like ball_touch the test is
 // conservative in f32 (a margin of 1e-5 of every magnitude involved), so it
 // never drops an object some lane's segment touches: results are unchanged.
+// Every lane of the wave active AT THIS POINT.  The transposed tests (lane j
+// tests object / leaf j for the whole wave) and the DPP / readlane bundle
+// reductions are valid only then, so each of them checks the exec mask where
+// it runs (a convergent read: __builtin_amdgcn_read_exec lowers to
+// llvm.amdgcn.ballot(true), which the compiler cannot move across control
+// flow) and otherwise falls back to the all-candidates mask.  Culling then
+// stays exact whatever the compiler does with the surrounding regions.
+__device__ __forceinline__ bool exec_full() { return __builtin_amdgcn_read_exec() == ~0ull; }
+
 __device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {   // every lane must be active
     // row_ror:1,2,4,8 (DPP) leaves each row's maximum in all its lanes
@@ -1524,7 +1533,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
     // without the capsule (a partially active wave, or unbounded / non-finite
     // segments) every object is a candidate and each bounded one gets the
     // per-lane segment test
-    const bool cap = wave_ok && !__any(need && !fin);
+    const bool cap = wave_ok && exec_full() && !__any(need && !fin);
     const int f = __builtin_ctzll(nm);
     const float ax = rdlane_f(Ax, f), ay = rdlane_f(Ay, f), az = rdlane_f(Az, f);
     const float bx = rdlane_f(Bx, f), by = rdlane_f(By, f), bz = rdlane_f(Bz, f);
@@ -1567,7 +1576,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
         const int nc = S.n_objs - base;
-        uint64_t m = cap ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        uint64_t m = (cap && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             if (need) {
@@ -1590,7 +1599,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             // otherwise the leaves whose balls no querying lane's line meets
             uint64_t lmask = ~0ull;
             bool use_mask = false;
-            if (cap && ob.npb > 0) {
+            if (cap && ob.npb > 0 && exec_full()) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
                 const bool in = lane < ob.npb;
                 if (!__any(in && capsule_touch(g, ax, ay, az, ux, uy, uz, uu, rho, mag))) {
@@ -1618,7 +1627,11 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
 #else
                 use_mask = lcth > 0.0f;
 #endif
-                if (use_mask) lmask = __ballot(in && line_touch(g, lox, loy, loz, lax, lay, laz, lcth, lsth, lrho, lmag));
+                if (use_mask) {
+                    const bool full = exec_full();
+                    const uint64_t b = __ballot(in && line_touch(g, lox, loy, loz, lax, lay, laz, lcth, lsth, lrho, lmag));
+                    lmask = full ? b : ~0ull;
+                }
             }
             if (S.cull && ob.has_bound) {   // per-lane segment test (f32, cheaper than an FP64 miss)
                 if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
@@ -1633,24 +1646,20 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_SH_HIT);
             if (csg_obj) cnt.ev(EV_SH_CSG);
-            if constexpr (std::is_same<CT, Cnt<false>>::value) {
+            {
                 // every lane evaluates (the wave runs the object anyway) and
                 // only querying lanes without a hit take the result: no
-                // divergent region between this loop's wave-wide tests (the
-                // lane-j-tests-object-j ballots need every lane active; with
-                // `if (need && !hit)` here, the backend's uniform-region
-                // structurization left the exec mask reduced for them and
-                // changed culled shadow decisions)
+                // divergent region between this loop's wave-wide tests.  The
+                // op-counting builds take the same path and count only the
+                // reference's calls (querying lanes without a hit yet).
                 real t = RV(0.0), ts = RV(0.0);
                 V3 p;
                 int code = 0;
+                const bool take = need && !hit;
+                cnt.gate(take);
                 const bool h = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt, lmask, use_mask);
-                hit = hit || (need && h);
-            } else if (need && !hit) {   // op-counting builds count only the reference's calls
-                real t = RV(0.0), ts = RV(0.0);
-                V3 p;
-                int code = 0;
-                hit = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt, lmask, use_mask);
+                cnt.gate(true);
+                hit = hit || (take && h);
             }
             cnt.pe(PH_OBJ_HIT);
             if (csg_obj) cnt.pe(PH_SHADOW_CSG);
@@ -1695,7 +1704,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     const bool fin = __builtin_isfinite(fr.ox + fr.oy + fr.oz + fr.dx + fr.dy + fr.dz);
     // no cone for a partially active wave or non-finite rays: every object is
     // a candidate (the per-lane ball test still runs)
-    const bool cone = S.cull && wave_ok && !__any(!fin) && tmin >= RV(0.0);
+    const bool cone = S.cull && wave_ok && exec_full() && !__any(!fin) && tmin >= RV(0.0);
     const float ox = rdlane_f(fr.ox, 0), oy = rdlane_f(fr.oy, 0), oz = rdlane_f(fr.oz, 0);
     const float ax = rdlane_f(fr.dx, 0), ay = rdlane_f(fr.dy, 0), az = rdlane_f(fr.dz, 0);
     const float do2 = (fr.ox - ox) * (fr.ox - ox) + (fr.oy - oy) * (fr.oy - oy) + (fr.oz - oz) * (fr.oz - oz);
@@ -1723,7 +1732,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             pass = type != 0 && (type != 2 || wide || cone_touch(c0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
         }
         const int nc = S.n_objs - base;
-        uint64_t m = cone ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        uint64_t m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             int skipped = 0;
@@ -1745,13 +1754,13 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             uint64_t lmask = ~0ull;
 #ifdef RT_NO_LEAF_MASK
             const bool use_mask = false;
-            if (!wide && ob.npb > 0 && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
+            if (!wide && ob.npb > 0 && exec_full() && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
                 cnt.inc(RT_OPC_CULLED);
                 cnt.pe(PH_OBJ_PREF);
                 continue;
             }
 #else
-            const bool use_mask = !wide && ob.npb > 0;
+            const bool use_mask = !wide && ob.npb > 0 && exec_full();
 #endif
             if (use_mask) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
@@ -1761,7 +1770,9 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                     cnt.pe(PH_OBJ_PREF);
                     continue;
                 }
-                lmask = __ballot(in && line_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+                const bool full = exec_full();
+                const uint64_t b = __ballot(in && line_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+                lmask = full ? b : ~0ull;
             }
             if (S.cull && ob.has_bound && !__any(ball_touch(ob.fb, fr, ftmin, (float)closest))) {
                 cnt.inc(RT_OPC_CULLED);

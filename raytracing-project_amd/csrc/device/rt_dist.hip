@@ -147,12 +147,15 @@ struct rt_dist {
     hipStream_t alt_st = nullptr;             // odd trace chunks (a chunk's tail overlaps the next chunk)
     DevBuf mine, mine8, stage, rowtab;
     hipEvent_t ev_chunk[kChunks] = {};
-    hipEvent_t ev_g0 = nullptr, ev_g1 = nullptr;
+    hipEvent_t ev_gs[kChunks] = {}, ev_ge[kChunks] = {};   // each collective + its placement (comm_st)
     hipEvent_t ev_alt = nullptr;              // end of alt_st's work in a frame (joined into st)
     hipEvent_t ev_tb[2 * kChunks] = {};
     std::vector<int32_t> rowtab_host;          // source of the async row-table upload
     std::mutex mu;                            // one frame at a time per rank
     DevBuf* sim_stage = nullptr;              // rt_test_render_dist_sim: shared stage, copies instead of RCCL
+    bool force_collective = false;            // rt_test_dist_create_rccl1: world 1 through ncclGather
+    DevBuf red;                               // rt_dist_reduce_max scratch
+    bool collective() const { return world > 1 || force_collective; }
 };
 
 namespace {
@@ -165,8 +168,8 @@ int dist_init_streams(rt_dist& D) {
     HIP_TRY(hipStreamCreateWithFlags(&D.alt_st, hipStreamNonBlocking));
     for (auto& e : D.ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : D.ev_tb) HIP_TRY(hipEventCreate(&e));
-    HIP_TRY(hipEventCreate(&D.ev_g0));
-    HIP_TRY(hipEventCreate(&D.ev_g1));
+    for (auto& e : D.ev_gs) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : D.ev_ge) HIP_TRY(hipEventCreate(&e));
     HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
     return RT_OK;
 }
@@ -190,13 +193,14 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     const int m = max_rows(H, D.world);
     const size_t row_elems = (size_t)W * 3;
     const size_t row_bytes = row_elems * (kind ? 1 : sizeof(double));
-    const auto bounds = chunk_bounds(m, D.world > 1 ? kChunks : 1);
-    const bool direct = D.world == 1 && kind == 0;   // trace straight into the caller's frame
+    const bool coll = D.collective();
+    const auto bounds = chunk_bounds(m, coll ? kChunks : 1);
+    const bool direct = !coll && kind == 0;   // trace straight into the caller's frame
     if (!direct) HIP_TRY(D.mine.ensure(std::max<size_t>(1, (size_t)m * row_elems * sizeof(double))));
-    if (kind == 1 && D.world > 1) HIP_TRY(D.mine8.ensure(std::max<size_t>(1, (size_t)m * row_elems)));
+    if (kind == 1 && coll) HIP_TRY(D.mine8.ensure(std::max<size_t>(1, (size_t)m * row_elems)));
     DevBuf& stage = D.sim_stage ? *D.sim_stage : D.stage;
-    if (D.world > 1 && (root || D.sim_stage)) HIP_TRY(stage.ensure((size_t)D.world * m * row_bytes));
-    if (D.world > 1 && root) {
+    if (coll && (root || D.sim_stage)) HIP_TRY(stage.ensure((size_t)D.world * m * row_bytes));
+    if (coll && root) {
         // placement table: chunk k occupies slots [world*a, world*b) as [rank][b-a]
         D.rowtab_host.assign((size_t)D.world * m, -1);
         for (int r = 0; r < D.world; ++r) {
@@ -214,27 +218,27 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     rc = rt_frame_begin(s, W, H, mode, flags, rows.data(), n, st, &f);
     if (rc != RT_OK) return rc;
     double* fb_rows = direct ? static_cast<double*>(out_root) : D.mine.as<double>();
-    int n_tb = 0;
-    if (D.world > 1) HIP_TRY(hipEventRecord(D.ev_g0, D.comm_st));
+    int n_tb = 0, n_g = 0;
     for (size_t k = 0; k < bounds.size() && rc == RT_OK; ++k) {
         const int a = bounds[k].first, b = bounds[k].second, hi = std::min(b, n);
         const hipStream_t cst = (k & 1) ? D.alt_st : st;   // chunks alternate between two streams
         if (hi > a) rc = rt_frame_trace(f, a, hi, fb_rows + (size_t)a * row_elems, cst);
         if (rc != RT_OK) break;
         if (kind == 1 && hi > a) {
-            uint8_t* dst8 = D.world > 1 ? D.mine8.as<uint8_t>() + (size_t)a * row_elems : static_cast<uint8_t*>(out_root);
+            uint8_t* dst8 = coll ? D.mine8.as<uint8_t>() + (size_t)a * row_elems : static_cast<uint8_t*>(out_root);
             if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) { rc = RT_ERR_HIP; break; }
             rc = rt_framebuffer_to_rgb8_device(fb_rows + (size_t)a * row_elems, (size_t)(hi - a) * W, dst8, cst);
             if (rc != RT_OK) break;
             if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) { rc = RT_ERR_HIP; break; }
         }
-        if (D.world == 1) continue;
+        if (!coll) continue;
         // chunk k -> root: ONE collective, ordered after the chunk's trace
         if (hipEventRecord(D.ev_chunk[k], cst) != hipSuccess || hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess) {
             rtamd::set_last_error("rt_render_dist: event chaining failed");
             rc = RT_ERR_HIP;
             break;
         }
+        if (hipEventRecord(D.ev_gs[n_g], D.comm_st) != hipSuccess) { rc = RT_ERR_HIP; break; }
         const char* send = (kind ? D.mine8.as<char>() : D.mine.as<char>()) + (size_t)a * row_bytes;
         const size_t chunk_bytes = (size_t)(b - a) * row_bytes;
         char* recv = stage.as<char>() + (size_t)D.world * a * row_bytes;
@@ -260,14 +264,14 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             rc = RT_ERR_HIP;
             break;
         }
+        if (hipEventRecord(D.ev_ge[n_g++], D.comm_st) != hipSuccess) { rc = RT_ERR_HIP; break; }
     }
-    if (D.world > 1) (void)hipEventRecord(D.ev_g1, D.comm_st);
     // alt_st's last work (a chunk's toByte) into st, which rt_frame_end synchronises
     if (hipEventRecord(D.ev_alt, D.alt_st) != hipSuccess || hipStreamWaitEvent(st, D.ev_alt, 0) != hipSuccess) {
         if (rc == RT_OK) rc = RT_ERR_HIP;
     }
     const int rc_end = rt_frame_end(f, stats);   // joins and synchronises the trace streams
-    if (D.world > 1 && hipStreamSynchronize(D.comm_st) != hipSuccess && rc == RT_OK) {
+    if (coll && hipStreamSynchronize(D.comm_st) != hipSuccess && rc == RT_OK) {
         rtamd::set_last_error("rt_render_dist: gather stream failed");
         rc = RT_ERR_HIP;
     }
@@ -275,7 +279,12 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     if (rc_end != RT_OK) return rc_end;
     if (stats) {
         float ms = 0.f;
-        if (D.world > 1 && hipEventElapsedTime(&ms, D.ev_g0, D.ev_g1) == hipSuccess) stats->ms_gather = ms;
+        // the collectives and placements themselves (each waits for its
+        // chunk's trace first; the waits are not counted)
+        double g = 0.0;
+        for (int i = 0; i < n_g; ++i)
+            if (hipEventElapsedTime(&ms, D.ev_gs[i], D.ev_ge[i]) == hipSuccess) g += ms;
+        stats->ms_gather = g;
         double tb = 0.0;
         for (int i = 0; i + 1 < n_tb; i += 2)
             if (hipEventElapsedTime(&ms, D.ev_tb[i], D.ev_tb[i + 1]) == hipSuccess) tb += ms;
@@ -286,8 +295,39 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     return RT_OK;
 }
 
+// Everything a rank holds on its device: the communicator (if owned),
+// buffers, streams and events.  The rank object itself stays valid (empty).
+void release_rank(rt_dist& d) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(d.device);
+    if (d.comm_st) (void)hipStreamSynchronize(d.comm_st);
+    if (d.comm && d.own_comm) (void)ncclCommDestroy(d.comm);
+    d.comm = nullptr;
+    d.own_comm = false;
+    d.mine.release();
+    d.mine8.release();
+    d.stage.release();
+    d.rowtab.release();
+    d.red.release();
+    if (d.comm_st) (void)hipStreamDestroy(d.comm_st);
+    if (d.alt_st) (void)hipStreamDestroy(d.alt_st);
+    d.comm_st = d.alt_st = nullptr;
+    auto drop = [](hipEvent_t& e) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    };
+    for (auto& e : d.ev_chunk) drop(e);
+    for (auto& e : d.ev_tb) drop(e);
+    for (auto& e : d.ev_gs) drop(e);
+    for (auto& e : d.ev_ge) drop(e);
+    drop(d.ev_alt);
+    (void)hipSetDevice(prev);
+}
+
 // --------------------------------------------- one process, n devices
 struct LocalGroup {
+    std::mutex mu;   // one rt_render_multi / rt_render_rgb8 call at a time per group (comms, root buffers)
     int n = 0;
     std::vector<std::unique_ptr<rt_dist>> ranks;
     DevBuf out;      // root frame (device 0)
@@ -296,6 +336,27 @@ struct LocalGroup {
 
 std::mutex g_groups_mu;
 std::map<int, std::unique_ptr<LocalGroup>> g_groups;
+
+// rt_shutdown: destroy every cached group (RCCL communicators, streams,
+// buffers).  Groups are created again on the next multi-GPU call.
+int shutdown_groups() {
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    int n = 0;
+    for (auto& kv : g_groups) {
+        LocalGroup& G = *kv.second;
+        std::lock_guard<std::mutex> glk(G.mu);
+        for (auto& r : G.ranks) release_rank(*r);
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(0);
+        G.out.release();
+        G.out8.release();
+        (void)hipSetDevice(prev);
+        ++n;
+    }
+    g_groups.clear();
+    return n;
+}
 
 int local_group(int n, LocalGroup** out) {
     std::lock_guard<std::mutex> lk(g_groups_mu);
@@ -348,6 +409,10 @@ int render_multi(const rt_scene* s, int W, int H, int mode, int flags, int n_gpu
     LocalGroup* G = nullptr;
     int rc = local_group(n, &G);
     if (rc != RT_OK) return rc;
+    // the whole call under the group's lock: buffer ensure, the per-device
+    // threads (their ncclGather calls must not interleave with another
+    // call's on the same communicators) and the D2H copy
+    std::lock_guard<std::mutex> glk(G->mu);
     const size_t out_bytes = (size_t)W * H * 3 * (kind ? 1 : sizeof(double));
     HIP_TRY(hipSetDevice(0));
     DevBuf& out = kind ? G->out8 : G->out;
@@ -460,22 +525,7 @@ extern "C" int rt_dist_create(const uint8_t id[RT_DIST_ID_BYTES], int world, int
 
 extern "C" void rt_dist_destroy(rt_dist* d) {
     if (!d) return;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(d->device);
-    if (d->comm && d->own_comm) (void)ncclCommDestroy(d->comm);
-    d->mine.release();
-    d->mine8.release();
-    d->stage.release();
-    d->rowtab.release();
-    if (d->comm_st) (void)hipStreamDestroy(d->comm_st);
-    for (auto e : d->ev_chunk) if (e) (void)hipEventDestroy(e);
-    for (auto e : d->ev_tb) if (e) (void)hipEventDestroy(e);
-    if (d->ev_g0) (void)hipEventDestroy(d->ev_g0);
-    if (d->ev_g1) (void)hipEventDestroy(d->ev_g1);
-    if (d->alt_st) (void)hipStreamDestroy(d->alt_st);
-    if (d->ev_alt) (void)hipEventDestroy(d->ev_alt);
-    (void)hipSetDevice(prev);
+    release_rank(*d);
     delete d;
 }
 
@@ -517,19 +567,84 @@ extern "C" int rt_test_render_dist_sim(const rt_scene* s, int W, int H, int mode
     }
     if (rc == RT_OK && hipMemcpy(rgb8 ? (void*)rgb8_host : (void*)fb_host, out.p, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
         rc = RT_ERR_HIP;
-    for (auto& d : ranks) {
-        d->mine.release();
-        d->mine8.release();
-        d->rowtab.release();
-        if (d->comm_st) (void)hipStreamDestroy(d->comm_st);
-        for (auto e : d->ev_chunk) if (e) (void)hipEventDestroy(e);
-        for (auto e : d->ev_tb) if (e) (void)hipEventDestroy(e);
-        if (d->ev_g0) (void)hipEventDestroy(d->ev_g0);
-        if (d->ev_g1) (void)hipEventDestroy(d->ev_g1);
-        if (d->alt_st) (void)hipStreamDestroy(d->alt_st);
-        if (d->ev_alt) (void)hipEventDestroy(d->ev_alt);
-    }
+    for (auto& d : ranks) release_rank(*d);
     stage.release();
     out.release();
     return rc;
+}
+
+// ---------------------------------------- launcher plumbing over RCCL
+// Max-reduction of a few doubles over every rank of d (host in, host out):
+// the bench's max-over-ranks timing and its barrier, for launchers without a
+// collective layer of their own.  World 1 without a communicator: identity.
+extern "C" int rt_dist_reduce_max(rt_dist* d, double* vals_host, int n) {
+    if (!d || n < 0 || (n > 0 && !vals_host)) { rtamd::set_last_error("rt_dist_reduce_max: bad arguments"); return RT_ERR_INVALID_ARG; }
+    if (!d->comm || n == 0) return RT_OK;
+    std::lock_guard<std::mutex> lk(d->mu);
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(d->device));
+    int rc = dist_init_streams(*d);
+    if (rc == RT_OK) {
+        const size_t bytes = (size_t)n * sizeof(double);
+        if (d->red.ensure(bytes) != hipSuccess ||
+            hipMemcpyAsync(d->red.p, vals_host, bytes, hipMemcpyHostToDevice, d->comm_st) != hipSuccess) {
+            rtamd::set_last_error("rt_dist_reduce_max: device buffer failed");
+            rc = RT_ERR_HIP;
+        } else {
+            const ncclResult_t r = ncclAllReduce(d->red.p, d->red.p, (size_t)n, ncclFloat64, ncclMax, d->comm, d->comm_st);
+            if (r != ncclSuccess) {
+                rtamd::set_last_error(std::string("ncclAllReduce failed: ") + ncclGetErrorString(r));
+                rc = RT_ERR_HIP;
+            } else if (hipMemcpyAsync(vals_host, d->red.p, bytes, hipMemcpyDeviceToHost, d->comm_st) != hipSuccess ||
+                       hipStreamSynchronize(d->comm_st) != hipSuccess) {
+                rtamd::set_last_error("rt_dist_reduce_max: copy back failed");
+                rc = RT_ERR_HIP;
+            }
+        }
+    }
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+extern "C" int rt_dist_barrier(rt_dist* d) {
+    double z = 0.0;
+    return rt_dist_reduce_max(d, &z, 1);
+}
+
+// Release every device resource the library caches: the per-device
+// workspaces of rt_render* (scene copies, jitter table, frame buffers) and
+// the device groups of rt_render_multi / rt_render_rgb8 (RCCL communicators,
+// streams, buffers).  rt_dist handles are the caller's (rt_dist_destroy).
+// No render may be in flight; later calls re-create what they need.
+extern "C" int rt_shutdown(void) {
+    shutdown_groups();
+    return rtamd::release_device_workspaces();
+}
+
+// ------------------------------------------------------------- test hook
+// A world-1 rank WITH a real RCCL communicator (ncclCommInitRank over one
+// rank) whose frames take the collective path: row chunks, ncclGather to
+// root 0, placement.  On a one-GPU machine this runs the collective API
+// surface of the multi-GPU frame (arguments, counts, datatypes, root, the
+// communicator's lifetime) through RCCL itself.
+extern "C" int rt_test_dist_create_rccl1(rt_dist** out) {
+    if (!out) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    uint8_t id[RT_DIST_ID_BYTES];
+    int rc = rt_dist_get_id(id);
+    if (rc != RT_OK) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
+    std::unique_ptr<rt_dist> D(new rt_dist);
+    D->world = 1;
+    D->rank = 0;
+    D->force_collective = true;
+    HIP_TRY(hipGetDevice(&D->device));
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    NCCL_TRY(ncclCommInitRank(&D->comm, 1, u, 0));
+    D->own_comm = true;
+    *out = D.release();
+    return RT_OK;
 }

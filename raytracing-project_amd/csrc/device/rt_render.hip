@@ -88,6 +88,11 @@ struct DBuf {
     }
     template <class T>
     T* as() const { return reinterpret_cast<T*>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
 };
 
 // The device-resident copy of one scene (compiled object table + records in
@@ -126,14 +131,20 @@ struct Workspace {
     SceneCache sc;
 };
 
+std::mutex g_ws_mu;
+std::vector<Workspace*> g_ws;   // per device; never deleted (frames hold pointers), emptied by rt_shutdown
+
 Workspace& workspace(int dev) {
-    static std::mutex gm;
-    static std::vector<Workspace*> ws;
-    std::lock_guard<std::mutex> lk(gm);
-    if ((int)ws.size() <= dev) ws.resize(dev + 1, nullptr);
-    if (!ws[dev]) ws[dev] = new Workspace;
-    return *ws[dev];
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    if ((int)g_ws.size() <= dev) g_ws.resize(dev + 1, nullptr);
+    if (!g_ws[dev]) g_ws[dev] = new Workspace;
+    return *g_ws[dev];
 }
+
+// rt_render's staging frame (host-output path), one per process
+std::mutex g_fb_mu;
+DBuf g_fb;
+int g_fb_dev = 0;
 
 template <class T>
 hipError_t upload(DBuf& b, const std::vector<T>& v, hipStream_t st) {
@@ -373,7 +384,12 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         int max_y = 0;
         for (int i = 0; i < n_rows; ++i) max_y = std::max(max_y, H - 1 - rows_host[i]);
         const int64_t q_end = (int64_t)32 * W * (max_y + 1);
-        HIP_TRY(ws.jtab.ensure((q_end - 1) / ((int64_t)rtamd::kTableK * 624) + 1, st));
+        try {   // (the jump polynomials: file read or GF(2) arithmetic, may throw)
+            HIP_TRY(ws.jtab.ensure((q_end - 1) / ((int64_t)rtamd::kTableK * 624) + 1, st));
+        } catch (const std::exception& e) {
+            rtamd::set_last_error(std::string("jitter checkpoint table: ") + e.what());
+            return RT_ERR_PROCESSING;
+        }
     }
     HIP_TRY(hipEventRecord(ws.ev[0], st));
     if (n_rows > 0 && mode == RT_MODE_STANDARD) {
@@ -590,11 +606,103 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
 
 }  // namespace
 
+int rtamd::release_device_workspaces() {
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess) return RT_ERR_NO_DEVICE;
+    {
+        std::lock_guard<std::mutex> lk(g_fb_mu);
+        if (g_fb.p) {
+            (void)hipSetDevice(g_fb_dev);
+            g_fb.release();
+        }
+    }
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (size_t dev = 0; dev < g_ws.size(); ++dev) {
+        Workspace* w = g_ws[dev];
+        if (!w) continue;
+        std::lock_guard<std::mutex> wl(w->mu);   // waits for an open frame of this device
+        (void)hipSetDevice((int)dev);
+        (void)hipDeviceSynchronize();
+        for (DBuf* b : {&w->nodes, &w->mats, &w->lights, &w->dlights, &w->objs, &w->ops, &w->gb, &w->ctab, &w->fold,
+                        &w->nodes_f, &w->mats_f, &w->lights_f, &w->dlights_f, &w->fold_f, &w->rows, &w->jit, &w->ckpt,
+                        &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb})
+            b->release();
+        w->jtab.release();
+        for (auto& e : w->ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
+        for (auto& e : w->tev)
+            if (e) (void)hipEventDestroy(e);
+        w->tev.clear();
+        w->sc = SceneCache();
+    }
+    (void)hipSetDevice(prev);
+    return RT_OK;
+}
+
 // ------------------------------------------------------------------ C-ABI
 extern "C" int rt_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+extern "C" int rt_set_device(int device) {
+    HIP_TRY(hipSetDevice(device));
+    return RT_OK;
+}
+
+extern "C" int rt_device_alloc(size_t bytes, void** dev_out) {
+    if (!dev_out) { rtamd::set_last_error("rt_device_alloc: NULL"); return RT_ERR_INVALID_ARG; }
+    *dev_out = nullptr;
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, bytes ? bytes : 1));
+    const hipError_t e = hipMemset(p, 0, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        rtamd::set_last_error(std::string("rt_device_alloc: hipMemset failed: ") + hipGetErrorString(e));
+        return RT_ERR_HIP;
+    }
+    *dev_out = p;
+    return RT_OK;
+}
+
+extern "C" int rt_device_free(void* dev) {
+    if (dev) HIP_TRY(hipFree(dev));
+    return RT_OK;
+}
+
+extern "C" int rt_memcpy_h2d(void* dev, const void* host, size_t bytes) {
+    if (!bytes) return RT_OK;
+    if (!dev || !host) { rtamd::set_last_error("rt_memcpy_h2d: NULL"); return RT_ERR_INVALID_ARG; }
+    HIP_TRY(hipMemcpy(dev, host, bytes, hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+extern "C" int rt_memcpy_d2h(void* host, const void* dev, size_t bytes) {
+    if (!bytes) return RT_OK;
+    if (!dev || !host) { rtamd::set_last_error("rt_memcpy_d2h: NULL"); return RT_ERR_INVALID_ARG; }
+    HIP_TRY(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+extern "C" int rt_device_synchronize(void) {
+    HIP_TRY(hipDeviceSynchronize());
+    return RT_OK;
+}
+
+extern "C" int rt_stream_create(void** stream_out) {
+    if (!stream_out) { rtamd::set_last_error("rt_stream_create: NULL"); return RT_ERR_INVALID_ARG; }
+    hipStream_t st = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    *stream_out = st;
+    return RT_OK;
+}
+
+extern "C" int rt_stream_destroy(void* stream) {
+    if (stream) HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return RT_OK;
 }
 
 extern "C" int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host,
@@ -626,11 +734,12 @@ extern "C" int rt_render(const rt_scene* s, int W, int H, int mode, int flags, d
     HIP_TRY(hipGetDevice(&dev));
     std::vector<int32_t> rows(H);
     for (int r = 0; r < H; ++r) rows[r] = r;
-    static std::mutex fbm;
-    static DBuf fb;
-    std::lock_guard<std::mutex> lk(fbm);
+    std::lock_guard<std::mutex> lk(g_fb_mu);
+    DBuf& fb = g_fb;
     const size_t bytes = (size_t)W * H * 3 * sizeof(double);
+    if (fb.p && g_fb_dev != dev) fb.release();   // (a staging frame lives on one device)
     HIP_TRY(fb.ensure(bytes));
+    g_fb_dev = dev;
     int rc = render_rows_impl(s, W, H, mode, flags, rows.data(), H, fb.as<double>(), nullptr, stats);
     if (rc != RT_OK) return rc;
     const auto t1 = std::chrono::steady_clock::now();

@@ -295,6 +295,16 @@ bool mt_load_tree_polys(const std::string& path, int K_blocks, int levels, std::
               std::fread(hdr, 4, 4, f) == 4 && (int)hdr[0] == K_blocks && (int)hdr[1] >= levels &&
               hdr[2] == (uint32_t)kPolyWords32;
     std::vector<uint32_t> all;
+    // the level count comes from the file: bound it (a jump of 64^16 blocks is
+    // far past any frame) and by the file's own size before sizing the buffer
+    constexpr uint32_t kMaxLevels = 16;
+    if (ok) {
+        long here = std::ftell(f);
+        ok = hdr[1] <= kMaxLevels && here >= 0 && std::fseek(f, 0, SEEK_END) == 0;
+        const long end = ok ? std::ftell(f) : -1;
+        ok = ok && end >= here && std::fseek(f, here, SEEK_SET) == 0 &&
+             (uint64_t)(end - here) == (uint64_t)hdr[1] * (kMTRadix - 1) * kPolyWords32 * 4 + 8;
+    }
     if (ok) {
         all.resize((size_t)hdr[1] * (kMTRadix - 1) * kPolyWords32);
         uint64_t sum = 0;

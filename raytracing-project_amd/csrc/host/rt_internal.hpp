@@ -14,4 +14,6 @@ bool node_depth_ok(const rt_scene_desc& d, int idx, int level, int* maxdepth);
 // Process-unique id of a scene handle (scenes are immutable after creation,
 // so a device copy keyed by it never goes stale).
 uint64_t scene_uid(const rt_scene* s);
+// librtamd: free every per-device workspace (rt_shutdown); returns an rt_status.
+int release_device_workspaces();
 }  // namespace rtamd

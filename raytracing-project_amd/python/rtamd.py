@@ -176,8 +176,56 @@ def amd_lib():
         lib.rt_dist_rows.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32)]
         lib.rt_test_render_dist_sim.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                 _dp, C.POINTER(C.c_uint8)]
+        lib.rt_dist_reduce_max.argtypes = [C.c_void_p, _dp, C.c_int]
+        lib.rt_dist_barrier.argtypes = [C.c_void_p]
+        lib.rt_set_device.argtypes = [C.c_int]
+        lib.rt_device_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+        lib.rt_device_free.argtypes = [C.c_void_p]
+        lib.rt_memcpy_h2d.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.rt_memcpy_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.rt_stream_create.argtypes = [C.POINTER(C.c_void_p)]
+        lib.rt_stream_destroy.argtypes = [C.c_void_p]
+        lib.rt_test_dist_create_rccl1.argtypes = [C.POINTER(C.c_void_p)]
+        check_one_hip_runtime()
         _amd = lib
     return _amd
+
+
+def mapped_libraries(stem: str) -> list[str]:
+    """Real paths of the shared objects whose file name starts with `stem`
+    mapped into this process (/proc/self/maps)."""
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6:
+                    path = parts[5].strip()
+                    if os.path.basename(path).startswith(stem):
+                        out.add(os.path.realpath(path))
+    except OSError:
+        return []
+    return sorted(out)
+
+
+ROCM_DIR = os.path.realpath(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+
+def check_one_hip_runtime() -> str:
+    """librtamd.so must run on ONE HIP runtime, the one `ray` and the
+    INTEGRATION binding use: /opt/rocm's.  A process that imported torch
+    first has torch's bundled runtime (same soname) already mapped, and
+    librtamd.so binds to it; loading torch afterwards maps a second runtime
+    (two runtimes torn down at exit aborted the process).  Raises in both
+    cases; returns the runtime's path."""
+    hips = mapped_libraries("libamdhip64.so")
+    if len(hips) > 1:
+        raise RuntimeError("two HIP runtimes mapped in this process: " + ", ".join(hips) +
+                           " (do not import torch in a process that uses librtamd.so)")
+    if hips and not hips[0].startswith(ROCM_DIR + os.sep):
+        raise RuntimeError(f"librtamd.so is bound to the HIP runtime {hips[0]}, not {ROCM_DIR}'s "
+                           "(was torch imported first?)")
+    return hips[0] if hips else ""
 
 
 def oracle_lib():
@@ -316,6 +364,76 @@ def with_dir_lights(scene: Scene, lights) -> Scene:
 
 def device_count() -> int:
     return int(amd_lib().rt_device_count())
+
+
+def _ok(rc: int, what: str):
+    if rc != RT_OK:
+        raise RTError(rc, f"{what}: {last_error()}")
+
+
+def set_device(dev: int):
+    _ok(amd_lib().rt_set_device(dev), "rt_set_device")
+
+
+def device_synchronize():
+    _ok(amd_lib().rt_device_synchronize(), "rt_device_synchronize")
+
+
+class DeviceBuffer:
+    """A device allocation made by librtamd.so itself (rt_device_alloc): the
+    tests and bench need no second HIP runtime (torch) for their buffers."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        _ok(amd_lib().rt_device_alloc(self.nbytes, C.byref(p)), "rt_device_alloc")
+        self.ptr = p
+
+    def to_host(self, dtype=np.float64, shape=None) -> np.ndarray:
+        out = np.empty(self.nbytes // np.dtype(dtype).itemsize, dtype=dtype)
+        _ok(amd_lib().rt_memcpy_d2h(out.ctypes.data_as(C.c_void_p), self.ptr, out.nbytes), "rt_memcpy_d2h")
+        return out.reshape(shape) if shape is not None else out
+
+    def from_host(self, arr: np.ndarray):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _ok(amd_lib().rt_memcpy_h2d(self.ptr, arr.ctypes.data_as(C.c_void_p), arr.nbytes), "rt_memcpy_h2d")
+
+    def free(self):
+        if self.ptr is not None and self.ptr.value:
+            amd_lib().rt_device_free(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Stream:
+    """A non-blocking HIP stream made by librtamd.so (rt_stream_create)."""
+
+    def __init__(self):
+        p = C.c_void_p()
+        _ok(amd_lib().rt_stream_create(C.byref(p)), "rt_stream_create")
+        self.handle = p
+
+    def destroy(self):
+        if self.handle is not None and self.handle.value:
+            amd_lib().rt_stream_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def shutdown():
+    """rt_shutdown: release every device resource the library caches."""
+    _ok(amd_lib().rt_shutdown(), "rt_shutdown")
 
 
 @dataclass

@@ -3,14 +3,11 @@ import sys
 
 import pytest
 
-# torch first: its bundled HIP runtime (soname libamdhip64.so.7, like
-# /opt/rocm's) is then the process's one runtime, as in bench.py and the
-# tools.  Loading librtamd.so first and torch later inside a test aborted
-# the process at exit (heap corruption in runtime teardown) on the GPU box.
-try:
-    import torch  # noqa: F401
-except ImportError:
-    pass
+# No torch in the test process: librtamd.so runs on /opt/rocm's HIP runtime
+# (the one the `ray` CLI and the INTEGRATION binding use), and every GPU test
+# gets its device buffers and streams from the library itself
+# (rtamd.DeviceBuffer / rtamd.Stream).  rtamd.amd_lib() refuses a process
+# with torch's bundled runtime mapped (two runtimes aborted at exit).
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PY = os.path.join(REPO, "raytracing-project_amd", "python")

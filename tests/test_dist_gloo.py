@@ -11,9 +11,14 @@ pins the partition / offset / gather / scatter logic, not the GPU kernels
 import os
 import socket
 
+import multiprocessing as mp
+
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+
+# torch is imported only inside the spawned ranks: the pytest process itself
+# keeps one HIP runtime (/opt/rocm's, the one librtamd.so binds; rtamd
+# refuses a process where torch's bundled runtime is mapped too).
 
 
 def _free_port():
@@ -65,7 +70,14 @@ def test_two_rank_strip_frame_matches_single(rt, tmp_path, mode):
 
     text, _ = scenes.config_json(4, dpi=12)   # 48x27 snorlax, 5 lights
     out = str(tmp_path / "frame.npy")
-    mp.start_processes(_worker, args=(2, _free_port(), text, mode, out), nprocs=2, join=True, start_method="spawn")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, text, mode, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     got = np.load(out)
     sc = rt.load_scene_from_json_text(text)
     want, _ = rt.oracle_render(sc, sc.width, sc.height, mode)
@@ -87,3 +99,40 @@ def test_strip_partition_covers_frame():
                 b = frame_dist.chunk_bounds(m, chunks)
                 assert b[0][0] == 0 and b[-1][1] == m
                 assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+
+
+def _rdv_worker(rank, tag, out):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "raytracing-project_amd", "python"))
+    import rendezvous
+
+    data = bytes(range(128)) if rank == 0 else None
+    got = rendezvous.share_bytes(rank, data, 128, tag=tag, timeout=60)
+    with open(f"{out}.{rank}", "wb") as f:
+        f.write(got)
+
+
+def test_rendezvous_hands_rank0_bytes_to_every_rank(tmp_path):
+    """bench.py's torch-free id exchange (rendezvous.share_bytes): three
+    processes, rank 0 publishing after the others start polling."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "raytracing-project_amd", "python"))
+    import rendezvous
+
+    tag = f"test_{os.getpid()}"
+    out = str(tmp_path / "got")
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rdv_worker, args=(r, tag, out)) for r in (2, 1, 0)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(3):
+        assert open(f"{out}.{r}", "rb").read() == bytes(range(128))
+    rendezvous.cleanup(0, tag=tag)
+    assert not os.path.exists(rendezvous._path(tag))

@@ -83,8 +83,6 @@ def test_render_rgb8_is_host_tobyte(gpu, name):
 
 @pytest.mark.gpu
 def test_device_tobyte_special_values(gpu):
-    import torch
-
     v = np.array([np.nan, -np.nan, np.inf, -np.inf, -1.0, -0.0, 0.0, 1e-300, 0.5 / 255, 1.5 / 255, 2.5 / 255,
                   127.5 / 255, 254.5 / 255, 0.999999, 1.0, 1.0000001, 7.0, 0.5, np.nextafter(0.5 / 255, 1.0),
                   np.nextafter(0.5 / 255, 0.0)], dtype=np.float64)
@@ -93,13 +91,13 @@ def test_device_tobyte_special_values(gpu):
     v = np.concatenate([v, halfway, rng.uniform(-0.2, 1.2, 3000)])
     v = np.pad(v, (0, (-len(v)) % 3))
     want = gpu.to_rgb8(v.reshape(-1, 1, 3)).reshape(-1)
-    d_in = torch.from_numpy(v).cuda()
-    d_out = torch.zeros(len(v), dtype=torch.uint8, device="cuda")
-    rc = gpu.amd_lib().rt_framebuffer_to_rgb8_device(C.c_void_p(d_in.data_ptr()), len(v) // 3,
-                                                     C.c_void_p(d_out.data_ptr()), None)
+    d_in = gpu.DeviceBuffer(v.nbytes)
+    d_in.from_host(v)
+    d_out = gpu.DeviceBuffer(len(v))
+    rc = gpu.amd_lib().rt_framebuffer_to_rgb8_device(d_in.ptr, len(v) // 3, d_out.ptr, None)
     assert rc == 0
-    torch.cuda.synchronize()
-    assert np.array_equal(d_out.cpu().numpy(), want)
+    gpu.device_synchronize()
+    assert np.array_equal(d_out.to_host(np.uint8), want)
 
 
 @pytest.mark.gpu
@@ -131,8 +129,6 @@ def test_dist_path_odd_frames(gpu, w, h, world, mode):
 @pytest.mark.gpu
 def test_dist_world1_is_rt_render(gpu):
     """One process per GPU with world 1: rt_dist_create / rt_render_dist."""
-    import torch
-
     sc, mode = _scene(gpu, "cfg4_std")
     W, H = sc.width, sc.height
     lib = gpu.amd_lib()
@@ -141,15 +137,16 @@ def test_dist_world1_is_rt_render(gpu):
     d = C.c_void_p()
     assert lib.rt_dist_create(uid, 1, 0, C.byref(d)) == 0, gpu.last_error()
     try:
-        out = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+        out = gpu.DeviceBuffer(H * W * 3 * 8)
         st = gpu.Stats()
-        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, C.c_void_p(out.data_ptr()), None, C.byref(st))
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, None, C.byref(st))
         assert rc == 0, gpu.last_error()
-        assert np.array_equal(out.cpu().numpy(), gpu.Tracer(sc, W, H, mode).render())
-        out8 = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
-        rc = lib.rt_render_dist_rgb8(d, sc.handle, W, H, mode, 0, C.c_void_p(out8.data_ptr()), None, C.byref(st))
+        fb = out.to_host(np.float64, (H, W, 3))
+        assert np.array_equal(fb, gpu.Tracer(sc, W, H, mode).render())
+        out8 = gpu.DeviceBuffer(H * W * 3)
+        rc = lib.rt_render_dist_rgb8(d, sc.handle, W, H, mode, 0, out8.ptr, None, C.byref(st))
         assert rc == 0, gpu.last_error()
-        assert np.array_equal(out8.cpu().numpy(), gpu.to_rgb8(out.cpu().numpy()))
+        assert np.array_equal(out8.to_host(np.uint8, (H, W, 3)), gpu.to_rgb8(fb))
     finally:
         lib.rt_dist_destroy(d)
 
@@ -176,3 +173,70 @@ def test_cli_stats_wall_clock_split(gpu, tmp_path):
     for k in ("ms_load", "ms_rng", "ms_kernel", "ms_gather", "ms_tobyte", "ms_d2h", "ms_render", "ms_png", "ms_main"):
         assert k in st and st[k] >= 0.0, k
     assert st["n_gpus"] == 1 and st["ms_kernel"] > 0 and st["ms_main"] >= st["ms_render"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg4_std", "cfg5_paper"])
+def test_rccl_world1_collective_path(gpu, name):
+    """The multi-GPU frame through RCCL itself on one GPU: a world-1
+    communicator (ncclCommInitRank over one rank) whose frames take the
+    collective path (4 row chunks, ncclGather to root 0 on the collective
+    stream, placement), bit-equal to rt_render in FP64 and RGB8; then the
+    launcher plumbing (ncclAllReduce max, barrier) and communicator teardown."""
+    sc, mode = _scene(gpu, name)
+    W, H = sc.width, sc.height
+    lib = gpu.amd_lib()
+    d = C.c_void_p()
+    assert lib.rt_test_dist_create_rccl1(C.byref(d)) == 0, gpu.last_error()
+    try:
+        want = gpu.Tracer(sc, W, H, mode).render()
+        out = gpu.DeviceBuffer(H * W * 3 * 8)
+        st = gpu.Stats()
+        for _ in range(2):   # second frame reuses the communicator and buffers
+            rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, None, C.byref(st))
+            assert rc == 0, gpu.last_error()
+            assert np.array_equal(out.to_host(np.float64, (H, W, 3)), want)
+        assert st.ms_gather > 0.0 and st.n_gpus == 1
+        out8 = gpu.DeviceBuffer(H * W * 3)
+        rc = lib.rt_render_dist_rgb8(d, sc.handle, W, H, mode, 0, out8.ptr, None, C.byref(st))
+        assert rc == 0, gpu.last_error()
+        assert np.array_equal(out8.to_host(np.uint8, (H, W, 3)), gpu.to_rgb8(want))
+        v = (C.c_double * 3)(3.0, -1.0, 2.5)
+        assert lib.rt_dist_reduce_max(d, v, 3) == 0, gpu.last_error()
+        assert list(v) == [3.0, -1.0, 2.5]
+        assert lib.rt_dist_barrier(d) == 0
+    finally:
+        lib.rt_dist_destroy(d)
+
+
+@pytest.mark.gpu
+def test_render_multi_all_visible_devices(gpu):
+    """rt_render_multi / rt_render_rgb8 over every visible device (RCCL
+    ncclCommInitAll + ncclGather) equal rt_render bit for bit."""
+    n = gpu.device_count()
+    if n < 2:
+        pytest.skip(f"{n} device visible: the n > 1 path needs more (the driver's 8-GPU node)")
+    for name in ("cfg4_std", "cfg5_paper"):
+        sc, mode = _scene(gpu, name)
+        W, H = sc.width, sc.height
+        want = gpu.Tracer(sc, W, H, mode).render()
+        st = gpu.Stats()
+        assert np.array_equal(gpu.render_multi(sc, W, H, mode, n, stats=st), want)
+        assert st.n_gpus == n
+        assert np.array_equal(gpu.render_rgb8(sc, W, H, mode, n), gpu.to_rgb8(want))
+    gpu.shutdown()
+
+
+@pytest.mark.gpu
+def test_shutdown_releases_and_recovers(gpu):
+    """rt_shutdown frees the cached device state (workspaces, resident scene,
+    jitter table, device groups); the next calls rebuild it and render the
+    same frames."""
+    sc, mode = _scene(gpu, "cfg4_std")
+    W, H = sc.width, sc.height
+    a = gpu.Tracer(sc, W, H, mode).render()
+    a8 = gpu.render_rgb8(sc, W, H, mode, 1)
+    gpu.shutdown()
+    gpu.shutdown()   # idempotent
+    assert np.array_equal(gpu.Tracer(sc, W, H, mode).render(), a)
+    assert np.array_equal(gpu.render_rgb8(sc, W, H, mode, 1), a8)

@@ -82,3 +82,16 @@ def test_config4_full_size_matches_oracle(gpu, flags):
 @pytest.mark.parametrize("key", ["penguin:0", "penguin:1", "pokeballs:0", "pokeballs:1", "snorlax:0", "snorlax:1"])
 def test_native_example_matches_oracle(gpu, key):
     _check(gpu, key)
+
+
+@pytest.mark.gpu
+def test_config4_counting_pass_with_cull(gpu):
+    """bench.py's executed-FLOP pass (RT_FLAG_COUNT_OPS, culling on) at the
+    bench frame: the same image and ray counts as the timed kernel's frame."""
+    sc, mode = _scene(gpu, "cfg4")
+    W, H = sc.width, sc.height
+    s0, s1 = gpu.Stats(), gpu.Stats()
+    a = gpu.Tracer(sc, W, H, mode).render(s0)
+    b = gpu.Tracer(sc, W, H, mode, flags=gpu.RT_FLAG_COUNT_OPS).render(s1)
+    assert (s0.rays_intersect, s0.rays_occluded) == (s1.rays_intersect, s1.rays_occluded)
+    assert np.array_equal(a, b)

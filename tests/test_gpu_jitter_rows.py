@@ -66,8 +66,6 @@ def test_jitter_stream_short_segments(gpu, K, q0, q1, first, count):
 def test_row_subset_matches_full_frame(gpu, mode):
     """rt_render_rows_device on interleaved 8-row strips (the multi-GPU split)
     reproduces the same rows of the full frame bit for bit."""
-    import torch
-
     import scenes
     rt = gpu
     text, _ = scenes.config_json(4, dpi=40)   # 160x90 snorlax, 5 lights
@@ -78,12 +76,11 @@ def test_row_subset_matches_full_frame(gpu, mode):
     for world in (2, 3, 5):
         for rank in range(world):
             rows = [r for s in range((H + 7) // 8) if s % world == rank for r in range(s * 8, min(H, s * 8 + 8))]
-            buf = torch.zeros((len(rows), W, 3), dtype=torch.float64, device="cuda")
+            buf = rt.DeviceBuffer(len(rows) * W * 3 * 8)
             rc = lib.rt_render_rows_device(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
-                                           C.c_void_p(buf.data_ptr()), None, None)
+                                           buf.ptr, None, None)
             assert rc == 0, rt.last_error()
-            torch.cuda.synchronize()
-            got = buf.cpu().numpy()
+            got = buf.to_host(np.float64, (len(rows), W, 3))
             assert np.array_equal(got, full[rows]), (world, rank)
 
 
@@ -91,8 +88,6 @@ def test_row_subset_matches_full_frame(gpu, mode):
 def test_unordered_row_subset_and_duplicates(gpu):
     """Rows in arbitrary order (jitter ranges sorted on the host, written to
     their own jitter row) match the full frame; a duplicated row is rejected."""
-    import torch
-
     import scenes
     rt = gpu
     text, _ = scenes.config_json(4, dpi=40)
@@ -102,15 +97,14 @@ def test_unordered_row_subset_and_duplicates(gpu):
     lib = rt.amd_lib()
     rng = np.random.default_rng(7)
     rows = [int(r) for r in rng.permutation(H)[: H // 3]]
-    buf = torch.zeros((len(rows), W, 3), dtype=torch.float64, device="cuda")
+    buf = rt.DeviceBuffer(len(rows) * W * 3 * 8)
     rc = lib.rt_render_rows_device(sc.handle, W, H, 0, 0, (C.c_int32 * len(rows))(*rows), len(rows),
-                                   C.c_void_p(buf.data_ptr()), None, None)
+                                   buf.ptr, None, None)
     assert rc == 0, rt.last_error()
-    torch.cuda.synchronize()
-    assert np.array_equal(buf.cpu().numpy(), full[rows])
+    assert np.array_equal(buf.to_host(np.float64, (len(rows), W, 3)), full[rows])
     dup = rows[:4] + rows[:1]
     rc = lib.rt_render_rows_device(sc.handle, W, H, 0, 0, (C.c_int32 * len(dup))(*dup), len(dup),
-                                   C.c_void_p(buf.data_ptr()), None, None)
+                                   buf.ptr, None, None)
     assert rc == rt.RT_ERR_INVALID_ARG
     assert "duplicate" in rt.last_error()
 
@@ -121,8 +115,6 @@ def test_frame_chunks_on_two_streams(gpu, mode):
     """rt_frame_begin / trace (chunks alternating between two HIP streams) /
     end reproduces the rows of the full frame bit for bit, with the same ray
     counts as one rt_render_rows_device call (the bench's multi-GPU path)."""
-    import torch
-
     import frame_dist
     import scenes
     rt = gpu
@@ -132,24 +124,24 @@ def test_frame_chunks_on_two_streams(gpu, mode):
     full = rt.Tracer(sc, W, H, mode).render()
     lib = rt.amd_lib()
     rows = frame_dist.strip_rows(H, 1, 3)
-    s0 = torch.cuda.current_stream()
-    streams = [s0, torch.cuda.Stream()]
-    buf = torch.zeros((len(rows), W, 3), dtype=torch.float64, device="cuda")
+    streams = [rt.Stream(), rt.Stream()]
+    row_bytes = W * 3 * 8
+    buf = rt.DeviceBuffer(len(rows) * row_bytes)
     fr = C.c_void_p()
     rc = lib.rt_frame_begin(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
-                            C.c_void_p(s0.cuda_stream), C.byref(fr))
+                            streams[0].handle, C.byref(fr))
     assert rc == 0, rt.last_error()
     for k, (a, b) in enumerate(frame_dist.chunk_bounds(len(rows), 5)):
-        rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf[a].data_ptr()), C.c_void_p(streams[k % 2].cuda_stream))
+        rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf.ptr.value + a * row_bytes), streams[k % 2].handle)
         assert rc == 0, rt.last_error()
     st = rt.Stats()
     assert lib.rt_frame_end(fr, C.byref(st)) == 0
-    torch.cuda.synchronize()
-    assert np.array_equal(buf.cpu().numpy(), full[rows])
+    rt.device_synchronize()
+    assert np.array_equal(buf.to_host(np.float64, (len(rows), W, 3)), full[rows])
     st1 = rt.Stats()
-    buf2 = torch.zeros_like(buf)
+    buf2 = rt.DeviceBuffer(len(rows) * row_bytes)
     rc = lib.rt_render_rows_device(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
-                                   C.c_void_p(buf2.data_ptr()), None, C.byref(st1))
+                                   buf2.ptr, None, C.byref(st1))
     assert rc == 0
     assert (st.rays_intersect, st.rays_occluded) == (st1.rays_intersect, st1.rays_occluded)
 

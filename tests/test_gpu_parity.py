@@ -149,3 +149,33 @@ def test_dir_lights_match_oracle(gpu, mode):
         if mode == 1:
             assert np.array_equal(fb, ref), name
         assert (st.rays_intersect, st.rays_occluded) == (ost.rays_intersect, ost.rays_occluded), name
+
+
+# The op-counting kernels (RT_FLAG_COUNT_OPS) take the timed kernels' control
+# flow (every lane evaluates each candidate object; counting is gated to the
+# reference's calls), so with culling ON they must render the same image and
+# count the same rays as the plain render.  bench.py's executed_frac comes
+# from exactly this pass.
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg4", "cfg5", "snorlax", "csg_groups", "reflect_refract", "csg_ops"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_counting_pass_with_cull_matches_plain(gpu, name, mode):
+    sc = gpu.load_scene_from_json_text(SMALL[name]())
+    W, H = sc.width, sc.height
+    s0, s1 = gpu.Stats(), gpu.Stats()
+    a = gpu.Tracer(sc, W, H, mode).render(s0)
+    b = gpu.Tracer(sc, W, H, mode, flags=gpu.RT_FLAG_COUNT_OPS).render(s1)
+    assert np.array_equal(a, b)
+    assert (s0.rays_intersect, s0.rays_occluded) == (s1.rays_intersect, s1.rays_occluded)
+    assert s1.ops[gpu.OP_NAMES.index("light_eval")] > 0
+
+
+@pytest.mark.gpu
+def test_counting_pass_with_cull_matches_plain_midres(gpu):
+    sc = gpu.load_scene_from_json_text(MID["cfg4_320"]())
+    W, H = sc.width, sc.height
+    s0, s1 = gpu.Stats(), gpu.Stats()
+    a = gpu.Tracer(sc, W, H, 0).render(s0)
+    b = gpu.Tracer(sc, W, H, 0, flags=gpu.RT_FLAG_COUNT_OPS).render(s1)
+    assert np.array_equal(a, b)
+    assert (s0.rays_intersect, s0.rays_occluded) == (s1.rays_intersect, s1.rays_occluded)

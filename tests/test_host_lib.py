@@ -32,7 +32,7 @@ def test_libraries_export_every_declared_symbol():
     assert len(declared) >= 18 and "rt_render" in declared and "rt_last_error" in declared
     for name in declared:
         assert hasattr(host, name) or hasattr(amd, name), name
-    assert amd.rt_abi_version() == 3
+    assert amd.rt_abi_version() == 4
 
 
 @pytest.mark.parametrize("H,world", [(2160, 8), (2160, 3), (1080, 2), (17, 4), (5, 8), (1, 1)])
@@ -154,3 +154,18 @@ def test_render_without_device_fails_loudly(rt):
     with pytest.raises(rt.RTError) as e:
         rt.Tracer(sc, 4, 4, 0).render()
     assert e.value.code == -7
+
+
+def test_runtime_guard_refuses_two_runtimes(rt, monkeypatch):
+    """rtamd.check_one_hip_runtime: a second HIP runtime (torch's bundled copy)
+    or a foreign one bound instead of /opt/rocm's is refused."""
+    rocm = rt.ROCM_DIR
+    monkeypatch.setattr(rt, "mapped_libraries",
+                        lambda stem: [rocm + "/lib/libamdhip64.so.7", "/x/torch/lib/libamdhip64.so"])
+    with pytest.raises(RuntimeError, match="two HIP runtimes"):
+        rt.check_one_hip_runtime()
+    monkeypatch.setattr(rt, "mapped_libraries", lambda stem: ["/x/torch/lib/libamdhip64.so"])
+    with pytest.raises(RuntimeError, match="not"):
+        rt.check_one_hip_runtime()
+    monkeypatch.setattr(rt, "mapped_libraries", lambda stem: [rocm + "/lib/libamdhip64.so.7"])
+    assert rt.check_one_hip_runtime().startswith(rocm)

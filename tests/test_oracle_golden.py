@@ -284,3 +284,16 @@ def test_oracle_deep_scenes_bit_exact(rt, mode):
         assert np.array_equal(fb, fr[f"{name}/{mode}/fb"]), name
         cnt = fr[f"{name}/{mode}/counts"]
         assert (st.rays_intersect, st.rays_occluded) == (int(cnt[0]), int(cnt[1])), name
+
+
+def test_oracle_cfg5_standard_960_counts_match_reference(rt):
+    """SURVEY.md §6 measured the reference on config 5's scene in STANDARD mode
+    at dpi 240 (960x540): 6,199,046 intersect + 28,798,014 occluded calls.
+    The oracle (the GPU tests' checker for the recursive path at scale)
+    reproduces them."""
+    import scenes
+
+    sc = rt.load_scene_from_json_text(scenes.config_json(5, dpi=240)[0])
+    assert (sc.width, sc.height) == (960, 540)
+    _, st = rt.oracle_render(sc, 960, 540, 0, threads=8)
+    assert (int(st.rays_intersect), int(st.rays_occluded)) == (6199046, 28798014)

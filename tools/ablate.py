@@ -11,7 +11,6 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
-import torch  # noqa: E402
 
 import rtamd  # noqa: E402
 import scenes  # noqa: E402
@@ -21,13 +20,13 @@ def run(name, scene, mode=0, flags=0, reps=2):
     sc = rtamd.load_scene_from_json_text(json.dumps(scene))
     W, H = sc.width, sc.height
     rows = list(range(H))
-    buf = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    buf = rtamd.DeviceBuffer(H * W * 3 * 8)
     lib = rtamd.amd_lib()
     st = rtamd.Stats()
     best = None
     for _ in range(reps):
         rc = lib.rt_render_rows_device(sc.handle, W, H, mode, flags, (C.c_int32 * H)(*rows), H,
-                                       C.c_void_p(buf.data_ptr()), None, C.byref(st))
+                                       buf.ptr, None, C.byref(st))
         assert rc == 0, rtamd.last_error()
         best = st.ms_kernel if best is None else min(best, st.ms_kernel)
     rays = st.rays_intersect + st.rays_occluded

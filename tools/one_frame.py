@@ -18,8 +18,6 @@ def main() -> int:
     ap.add_argument("--frames", type=int, default=2)
     ap.add_argument("--flags", type=int, default=0)
     a = ap.parse_args()
-    import torch
-
     import rtamd
     import scenes
 
@@ -31,13 +29,15 @@ def main() -> int:
     d = C.c_void_p()
     if lib.rt_dist_get_id(uid) != 0 or lib.rt_dist_create(uid, 1, 0, C.byref(d)) != 0:
         raise RuntimeError(rtamd.last_error())
-    out = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    out = rtamd.DeviceBuffer(H * W * 3 * 8)
     st = rtamd.Stats()
     for _ in range(a.frames):
-        if lib.rt_render_dist(d, sc.handle, W, H, mode, a.flags, C.c_void_p(out.data_ptr()), None, C.byref(st)) != 0:
+        if lib.rt_render_dist(d, sc.handle, W, H, mode, a.flags, out.ptr, None, C.byref(st)) != 0:
             raise RuntimeError(rtamd.last_error())
-    torch.cuda.synchronize()
+    rtamd.device_synchronize()
+    out.free()
     lib.rt_dist_destroy(d)
+    rtamd.shutdown()
     return 0
 
 

@@ -10,7 +10,6 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
-import torch  # noqa: E402
 
 import rtamd  # noqa: E402
 import scenes  # noqa: E402
@@ -21,11 +20,11 @@ def main():
     text, mode = scenes.config_json(cfg)[0], scenes.config_json(cfg)[1]
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
-    buf = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    buf = rtamd.DeviceBuffer(H * W * 3 * 8)
     st = rtamd.Stats()
     lib = rtamd.amd_lib()
     rc = lib.rt_render_rows_device(sc.handle, W, H, mode, rtamd.RT_FLAG_COUNT_OPS, (C.c_int32 * H)(*range(H)), H,
-                                   C.c_void_p(buf.data_ptr()), None, C.byref(st))
+                                   buf.ptr, None, C.byref(st))
     assert rc == 0, rtamd.last_error()
     d = st.as_dict() if hasattr(st, "as_dict") else None
     rays = st.rays_intersect + st.rays_occluded

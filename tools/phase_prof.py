@@ -13,7 +13,6 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
-import torch  # noqa: E402,F401
 
 import rtamd  # noqa: E402
 import scenes  # noqa: E402
@@ -27,12 +26,12 @@ def main():
     text, mode = scenes.config_json(cfg)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
-    buf = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    buf = rtamd.DeviceBuffer(H * W * 3 * 8)
     lib = rtamd.amd_lib()
     rows = (C.c_int32 * H)(*range(H))
     st = rtamd.Stats()
     for _ in range(3):
-        rc = lib.rt_render_rows_device(sc.handle, W, H, mode, 0, rows, H, C.c_void_p(buf.data_ptr()), None,
+        rc = lib.rt_render_rows_device(sc.handle, W, H, mode, 0, rows, H, buf.ptr, None,
                                        C.byref(st))
         assert rc == 0, rtamd.last_error()
     ph = [int(st.ops[k]) for k in range(len(PHASES))]

@@ -12,7 +12,6 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
-import torch  # noqa: E402
 
 import rtamd  # noqa: E402
 import scenes  # noqa: E402
@@ -33,11 +32,11 @@ def variant(name):
 def main():
     sc = rtamd.load_scene_from_json_text(json.dumps(variant(sys.argv[1])))
     W, H = sc.width, sc.height
-    buf = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    buf = rtamd.DeviceBuffer(H * W * 3 * 8)
     st = rtamd.Stats()
     for _ in range(2):
         rc = rtamd.amd_lib().rt_render_rows_device(sc.handle, W, H, 0, 0, (C.c_int32 * H)(*range(H)), H,
-                                                   C.c_void_p(buf.data_ptr()), None, C.byref(st))
+                                                   buf.ptr, None, C.byref(st))
         assert rc == 0, rtamd.last_error()
     print(sys.argv[1], "kernel ms", st.ms_kernel)
 
