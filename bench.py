@@ -300,9 +300,12 @@ def main() -> int:
                 r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
                 wall["cli_total"] = round((time.perf_counter() - tc) * 1e3, 3)
                 if r.returncode == 0:
-                    cs = json.loads(r.stdout.strip().splitlines()[-1])
+                    lines = r.stdout.strip().splitlines()
+                    cs = json.loads(lines[-1])
                     wall["cli_split"] = {k: cs[k] for k in ("ms_load", "ms_rng", "ms_kernel", "ms_tobyte", "ms_d2h",
                                                             "ms_render", "ms_png", "ms_main")}
+                    if len(lines) >= 2 and lines[-2].startswith("{"):
+                        wall["cli_setup"] = json.loads(lines[-2])   # one-time costs inside ms_render
                 else:
                     wall["cli_error"] = r.stderr[-300:]
         wall["note"] = ("cli_total = the `ray` process end to end (HIP init, JSON load, first-frame device "

@@ -342,6 +342,12 @@ int rt_memcpy_d2h(void* host, const void* dev, size_t bytes);
 int rt_device_synchronize(void);
 int rt_stream_create(void** stream_out);             /* non-blocking HIP stream              */
 int rt_stream_destroy(void* stream);
+/* One-time setup costs of this process so far, host wall clock in ms:
+ * out[0] scene compile + upload (first frame of each scene), out[1] jitter
+ * checkpoint-table builds / extensions, out[2] first trace-kernel launch
+ * (loads the kernels' code object onto the device), out[3] first jitter-fill
+ * launch (its code object).  n <= 4 entries are written. */
+int rt_setup_times(double* out, int n);
 /* Release every device resource the library caches (per-device workspaces,
  * resident scenes and jitter tables, the rt_render_multi device groups with
  * their RCCL communicators).  No render may be in flight; later calls

@@ -69,6 +69,10 @@ int main(int argc, char** argv) {
     tracer.n_gpus = n_gpus;
     if (fp32) tracer.flags |= RT_FLAG_FP32;
 
+    // HIP runtime initialisation (the first HIP call of the process), timed on its own for --stats
+    const auto t_hip0 = std::chrono::steady_clock::now();
+    (void)rt_device_count();
+    const auto t_hip1 = std::chrono::steady_clock::now();
     if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";
     std::vector<uint8_t> rgb;
@@ -99,6 +103,12 @@ int main(int argc, char** argv) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const double ms_render = ms(t0, t1);
         const double rays = (double)(s.rays_intersect + s.rays_occluded);
+        double setup[4] = {0, 0, 0, 0};
+        (void)rt_setup_times(setup, 4);
+        std::printf(
+            "{\"ms_hip_init\": %.3f, \"ms_setup_scene\": %.3f, \"ms_setup_jtable\": %.3f, "
+            "\"ms_setup_trace_load\": %.3f, \"ms_setup_jitter_load\": %.3f}\n",
+            ms(t_hip0, t_hip1), setup[0], setup[1], setup[2], setup[3]);
         std::printf(
             "{\"rays_intersect\": %llu, \"rays_occluded\": %llu, \"rays_traced\": %llu, \"n_gpus\": %d, "
             "\"ms_load\": %.3f, \"ms_rng\": %.3f, \"ms_kernel\": %.3f, \"ms_gather\": %.3f, \"ms_tobyte\": %.3f, "

@@ -141,6 +141,19 @@ Workspace& workspace(int dev) {
     return *g_ws[dev];
 }
 
+// One-time setup costs of this process (rt_setup_times): host wall time of
+// the scene compile + upload enqueue, the jitter checkpoint-table builds, and
+// the first launch of the trace kernels and of the jitter fill (a code
+// object is loaded onto the device at its first kernel launch).
+struct SetupTimes {
+    std::mutex mu;
+    double scene_ms = 0.0, jtable_ms = 0.0, trace_launch_ms = 0.0, jitter_launch_ms = 0.0;
+    bool trace_launched = false, jitter_launched = false;
+};
+SetupTimes g_setup;
+using SClock = std::chrono::steady_clock;
+double ms_since(SClock::time_point t) { return std::chrono::duration<double, std::milli>(SClock::now() - t).count(); }
+
 // rt_render's staging frame (host-output path), one per process
 std::mutex g_fb_mu;
 DBuf g_fb;
@@ -269,6 +282,14 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     SceneCache& sc = ws.sc;
     if (!sc.valid || sc.uid != rtamd::scene_uid(s) || sc.fp32 != fp32) {
         // compile + upload the scene once; later frames of it find it resident
+        const auto t_sc = SClock::now();
+        struct AddTime {
+            SClock::time_point t;
+            ~AddTime() {
+                std::lock_guard<std::mutex> lk(g_setup.mu);
+                g_setup.scene_ms += ms_since(t);
+            }
+        } add_scene_time{t_sc};
         sc.valid = false;
         try {
             sc.cs = rtamd::compile_scene(d);
@@ -385,7 +406,13 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         for (int i = 0; i < n_rows; ++i) max_y = std::max(max_y, H - 1 - rows_host[i]);
         const int64_t q_end = (int64_t)32 * W * (max_y + 1);
         try {   // (the jump polynomials: file read or GF(2) arithmetic, may throw)
-            HIP_TRY(ws.jtab.ensure((q_end - 1) / ((int64_t)rtamd::kTableK * 624) + 1, st));
+            const int64_t n_need = (q_end - 1) / ((int64_t)rtamd::kTableK * 624) + 1;
+            if (n_need > ws.jtab.n_ck) {   // a build or an extension: synchronous
+                const auto t_j = SClock::now();
+                HIP_TRY(ws.jtab.ensure(n_need, st));
+                std::lock_guard<std::mutex> lk(g_setup.mu);
+                g_setup.jtable_ms += ms_since(t_j);
+            }
         } catch (const std::exception& e) {
             rtamd::set_last_error(std::string("jitter checkpoint table: ") + e.what());
             return RT_ERR_PROCESSING;
@@ -417,7 +444,13 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(ws.jit.ensure((size_t)n_rows * 16 * W * sizeof(double)));
         HIP_TRY(ws.jscratch.ensure(rtamd::mt_fill_scratch_bytes(ws.jranges)));
         HIP_TRY(upload(ws.rows, f->rows_jrow, st));
+        const auto t_l = SClock::now();
         HIP_TRY(rtamd::mt_launch_fill(ws.jtab, ws.jranges, ws.jjob, ws.jscratch.p, ws.jit.as<double>(), st));
+        {
+            std::lock_guard<std::mutex> lk(g_setup.mu);
+            if (!g_setup.jitter_launched) g_setup.jitter_launch_ms = ms_since(t_l);
+            g_setup.jitter_launched = true;
+        }
         (void)q1;
     } else if (n_rows > 0) {
         // rows needing a primary hit: rendered rows and their vertical neighbours
@@ -478,6 +511,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
     // another stream first waits for the scene upload and jitter (begin); in
     // paper mode a chunk also reads primary hits an earlier chunk computed,
     // so chunks on different streams are chained
+    const auto t_launch = SClock::now();
     if (st != f->st) HIP_TRY(hipStreamWaitEvent(st, ws.ev[1], 0));
     if (f->mode == RT_MODE_PAPER && f->n_tev > 0 && f->last_st != st)
         HIP_TRY(hipStreamWaitEvent(st, ws.tev[f->n_tev - 1], 0));
@@ -549,6 +583,11 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         if (f->fp32) rtf::launch_paper_finish(g2, st, P);
         else rtd::launch_paper_finish(g2, st, P);
         HIP_TRY(hipGetLastError());
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_setup.mu);
+        if (!g_setup.trace_launched) g_setup.trace_launch_ms = ms_since(t_launch);
+        g_setup.trace_launched = true;
     }
     if ((int)ws.tev.size() <= f->n_tev) {
         hipEvent_t e = nullptr;
@@ -646,6 +685,14 @@ extern "C" int rt_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+extern "C" int rt_setup_times(double* out, int n) {
+    if (!out || n < 0) return RT_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(g_setup.mu);
+    const double v[4] = {g_setup.scene_ms, g_setup.jtable_ms, g_setup.trace_launch_ms, g_setup.jitter_launch_ms};
+    for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+    return RT_OK;
 }
 
 extern "C" int rt_set_device(int device) {

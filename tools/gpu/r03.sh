@@ -1,0 +1,20 @@
+# Round-3 evidence run: full GPU suite (one process, no torch), smoke, bench line,
+# rocprofv3 kernel-trace summary of a short bench run.
+# Usage (GPU box): TAG=r03a bash tools/gpu/r03.sh
+set -o pipefail
+export TMPDIR=/tmp
+T=${TAG:-r03}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error|assert" gpurun_out/${T}_gpu_tests.log | head -30; tail -30 gpurun_out/${T}_gpu_tests.log; exit 1; }
+tail -2 gpurun_out/${T}_gpu_tests.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/${T}_smoke.log; exit 1; }
+tail -1 gpurun_out/${T}_smoke.log
+timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { echo bench failed; tail gpurun_out/${T}_bench.err; exit 1; }
+tail -1 gpurun_out/${T}_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o run --output-format csv -- python bench.py --steps 50 --no-pmc --no-cpu --no-cli --fp32-steps 0 > gpurun_out/${T}_prof_bench.json 2>gpurun_out/${T}_prof.err || { echo prof failed; tail gpurun_out/${T}_prof.err; exit 1; }
+find gpurun_out/${T}_prof -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} gpurun_out/${T}_kernel_stats.csv
+head -8 gpurun_out/${T}_kernel_stats.csv
+# diagnostics (phase timers + wave event counts of the trace kernel), if the exp libraries were built
+if [ -f raytracing-project_amd/lib/exp/librtamd_prof.so ]; then
+  CFGS="4" timeout -k 10 200 bash tools/gpu/phase.sh prof > gpurun_out/${T}_phase.txt 2>&1 || echo "phase failed"
+  RTAMD_LIB=$PWD/raytracing-project_amd/lib/exp/librtamd_ev.so timeout -k 10 120 python tools/event_prof.py 4 > gpurun_out/${T}_events.txt 2>&1 || echo "events failed"
+fi
