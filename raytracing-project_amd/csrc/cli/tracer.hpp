@@ -93,7 +93,7 @@ struct Tracer {
     // device: rgb[(y*W + x)*3 + c], RGB order, top row first.
     void render_rgb8(std::vector<uint8_t>& rgb) const {
         if (!scene || !scene->get() || !camera || width <= 0 || height <= 0) return;
-        rgb.assign((size_t)width * height * 3, 0);
+        if (rgb.size() != (size_t)width * height * 3) rgb.assign((size_t)width * height * 3, 0);
         int rc = rt_render_rgb8(scene->get(), width, height,
                                 mode == RenderMode::Paper ? RT_MODE_PAPER : RT_MODE_STANDARD, flags, n_gpus,
                                 rgb.data(), &stats);

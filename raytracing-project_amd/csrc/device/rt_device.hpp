@@ -1514,31 +1514,62 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
     for (int i = 0; i < n; ++i) cnt.inc(k);
 }
 
+// Lane j's transposed test of object j's cull record (CompiledScene::ctab)
+// against the capsule of radius rho around the segment [a, b] (u = b - a).
+__device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, float ax, float ay, float az, float bx,
+                                             float by, float bz, float ux, float uy, float uz, float uu, float rho,
+                                             float mag) {
+    const int type = __float_as_int(c1.x);
+    if (type == 3) {
+        // a bare half-space: the segments cross its plane only if the capsule
+        // does (both axis ends farther than rho on one side: no lane); n.x - n.p
+        // in f32 is within 1e-6 of the magnitudes of the signed distance, far
+        // inside the margin
+        const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
+        const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
+        const float m = rho + 1e-5f * (mag + c1.y);
+        return !((sa > m && sb > m) || (sa < -m && sb < -m));   // NaN passes
+    }
+    return type == 1 || (type == 2 && capsule_touch(c0, ax, ay, az, ux, uy, uz, uu, rho, mag));
+}
+
 // Scene::occluded for the querying lanes of a fully active wave.  Returns
 // false for lanes with need = false.
+//
+// r0 is the shadow ray BEFORE the Ray constructor's re-normalisation of its
+// direction (core.h:278): the f32 culling works on it directly (the
+// re-normalised direction differs by a few FP64 ulps, far inside every cull
+// test's 1e-5 margins), and the exact FP64 ray (make_ray, one sqrt and three
+// divisions per lane) is formed only when some candidate object survives the
+// culls and is evaluated - most shadow queries of a wave end before that.
 template <bool EAGER, bool DEEP, bool UO, class CT>
-__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin, real tmax, bool need, bool wave_ok,
+__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
+#if defined(RT_ABL) && RT_ABL == 1   // diagnostic ablation builds only (wrong images): no shadow queries
+    return false;
+#endif
     cnt.pb(PH_WAVE_SETUP);
-    const FRay fr = to_fray(r);
+    const FRay fr = to_fray(r0);
+    DRay r = r0;           // the exact ray, formed on the first object evaluation (wave-uniform)
+    bool r_exact = false;
     const float ftmin = (float)tmin, ftmax = (float)tmax;
+    const uint64_t nm = __ballot(need);
+    if (!nm) return false;
+    cnt.ev(EV_SHQ);
+    const int f = __builtin_ctzll(nm);
     const float Ax = __builtin_fmaf(ftmin, fr.dx, fr.ox), Ay = __builtin_fmaf(ftmin, fr.dy, fr.oy),
                 Az = __builtin_fmaf(ftmin, fr.dz, fr.oz);
     const float Bx = __builtin_fmaf(ftmax, fr.dx, fr.ox), By = __builtin_fmaf(ftmax, fr.dy, fr.oy),
                 Bz = __builtin_fmaf(ftmax, fr.dz, fr.oz);
     const bool fin = __builtin_isfinite(Ax + Ay + Az + Bx + By + Bz);
-    const uint64_t nm = __ballot(need);
-    if (!nm) return false;
-    cnt.ev(EV_SHQ);
     // without the capsule (a partially active wave, or unbounded / non-finite
     // segments) every object is a candidate and each bounded one gets the
     // per-lane segment test
     const bool cap = wave_ok && exec_full() && !__any(need && !fin);
-    const int f = __builtin_ctzll(nm);
     const float ax = rdlane_f(Ax, f), ay = rdlane_f(Ay, f), az = rdlane_f(Az, f);
     const float bx = rdlane_f(Bx, f), by = rdlane_f(By, f), bz = rdlane_f(Bz, f);
-    float da = (Ax - ax) * (Ax - ax) + (Ay - ay) * (Ay - ay) + (Az - az) * (Az - az);
-    float db = (Bx - bx) * (Bx - bx) + (By - by) * (By - by) + (Bz - bz) * (Bz - bz);
+    const float da = (Ax - ax) * (Ax - ax) + (Ay - ay) * (Ay - ay) + (Az - az) * (Az - az);
+    const float db = (Bx - bx) * (Bx - bx) + (By - by) * (By - by) + (Bz - bz) * (Bz - bz);
     const float d = need ? __builtin_fmaxf(da, db) : 0.0f;
     const float rho = uni<UO>(cap ? sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(d)))) : 0.0f);
     const float ux = uni<UO>(bx - ax), uy = uni<UO>(by - ay), uz = uni<UO>(bz - az);
@@ -1552,32 +1583,22 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
     float lrho = 0.0f, lcth = -1.0f, lsth = 1.0f, lmag = 0.0f;
     bool hit = false;
     for (int base = 0; base < S.n_objs; base += 64) {
+        const int nc = S.n_objs - base;
         const int j = base + lane;
         bool pass = false;
         if (j < S.n_objs) {
             // the object's cull record (CompiledScene::ctab): one 32-byte load
             const float4 c0 = S.ctab[2 * j], c1 = S.ctab[2 * j + 1];
-            const int type = __float_as_int(c1.x);
-            if (!cap) {
-                pass = type != 0;
-            } else if (type == 3) {
-                // a bare half-space: the segments cross its plane only if the
-                // capsule does (both axis ends farther than rho on one side: no
-                // lane); n.x - n.p in f32 is within 1e-6 of the magnitudes of the
-                // signed distance, far inside the margin
-                const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
-                const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
-                const float m = rho + 1e-5f * (mag + c1.y);
-                pass = !((sa > m && sb > m) || (sa < -m && sb < -m));   // NaN passes
-            } else {
-                pass = type == 1 || (type == 2 && capsule_touch(c0, ax, ay, az, ux, uy, uz, uu, rho, mag));
-            }
+            pass = cap ? record_touch(c0, c1, ax, ay, az, bx, by, bz, ux, uy, uz, uu, rho, mag)
+                       : __float_as_int(c1.x) != 0;
         }
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
-        const int nc = S.n_objs - base;
         uint64_t m = (cap && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
+#if defined(RT_ABL) && RT_ABL == 2   // diagnostic: setup + transposed test only
+        if (m != 12345) return false;
+#endif
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             if (need) {
                 int skipped = 0;
@@ -1641,11 +1662,18 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r, real tmin,
                 }
             }
             cnt.pe(PH_OBJ_PREF);
+#if defined(RT_ABL) && RT_ABL == 3   // diagnostic: everything but the shadow object evaluations
+            if (m != 12345) continue;
+#endif
             const bool csg_obj = ob.kind == rtamd::OBJ_CHAIN && ob.core != 0;
             if (csg_obj) cnt.pb(PH_SHADOW_CSG);
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_SH_HIT);
             if (csg_obj) cnt.ev(EV_SH_CSG);
+            if (!r_exact) {   // Ray::Ray (core.h:278) of the shadow ray (shading.cpp:98), in place
+                r.d = normalized(r.d);
+                r_exact = true;
+            }
             {
                 // every lane evaluates (the wave runs the object anyway) and
                 // only querying lanes without a hit take the result: no
@@ -1949,13 +1977,14 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             if (!__any(need)) continue;
             cnt.ev(EV_LIGHT1);
             const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
-            const DRay sr = make_ray(so, wi);
             bool occ = false;
             if constexpr (WV) {
                 cnt.pb(PH_SHADOW);
-                occ = scene_occluded_wave<EAGER, DEEP, UO>(S, sr, eps, max_t, need, wave_full, cnt);
+                // (the direction's re-normalisation happens inside, when needed)
+                occ = scene_occluded_wave<EAGER, DEEP, UO>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
                 cnt.pe(PH_SHADOW);
             } else {
+                const DRay sr = make_ray(so, wi);
                 if (need) occ = scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt);
             }
             if (need) {
@@ -1967,6 +1996,9 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             cnt.pe(PH_SHADE1);
             cnt.pb(PH_SHADE2);
         }
+#if defined(RT_ABL) && RT_ABL == 4   // diagnostic: no pass-2 accumulation
+        if (lit != 12345u) continue;
+#endif
         if (!lit) continue;
         const MatT* m = &S.mats[hit.mat];
         const real kd = m->kd, ks = m->ks, shin = m->shininess;
@@ -2044,6 +2076,9 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
                                                                __builtin_amdgcn_read_exec() == ~0ull, cnt);
             cnt.pe(PH_PRIMARY);
             if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+#if defined(RT_ABL) && RT_ABL == 5   // diagnostic: primary hit only, no shading
+            if (S.n_objs != 12345) return hit ? h.n : v3(S.bg[0], S.bg[1], S.bg[2]);
+#endif
             const V3 E = shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, hit);
             return hit ? E : v3(S.bg[0], S.bg[1], S.bg[2]);
         } else {

@@ -26,7 +26,7 @@ import time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "raytracing-project_amd", "python"))
 
-import torch  # noqa: E402
+import numpy as np  # noqa: E402
 
 import frame_dist  # noqa: E402
 import rtamd  # noqa: E402
@@ -49,24 +49,25 @@ def main():
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
     lib = rtamd.amd_lib()
-    buf = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
-    stream = torch.cuda.current_stream()
-    streams = [stream, torch.cuda.Stream()] if args.two_streams else [stream]
+    row_bytes = W * 3 * 8
+    buf = rtamd.DeviceBuffer(H * row_bytes)
+    stream = rtamd.Stream()
+    streams = [stream, rtamd.Stream()] if args.two_streams else [stream]
     st = rtamd.Stats()
 
     def run(rows):
         if args.chunks <= 1:
             rc = lib.rt_render_rows_device(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
-                                           C.c_void_p(buf.data_ptr()), C.c_void_p(stream.cuda_stream), C.byref(st))
+                                           buf.ptr, stream.handle, C.byref(st))
             assert rc == 0, rtamd.last_error()
             return
         fr = C.c_void_p()
         rc = lib.rt_frame_begin(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
-                                C.c_void_p(stream.cuda_stream), C.byref(fr))
+                                stream.handle, C.byref(fr))
         assert rc == 0, rtamd.last_error()
         for k, (a, b) in enumerate(frame_dist.chunk_bounds(len(rows), args.chunks)):
             s = streams[k % len(streams)]
-            rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf[a].data_ptr()), C.c_void_p(s.cuda_stream))
+            rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf.ptr.value + a * row_bytes), s.handle)
             assert rc == 0, rtamd.last_error()
         rc = lib.rt_frame_end(fr, C.byref(st))
         assert rc == 0, rtamd.last_error()
@@ -79,10 +80,10 @@ def main():
             run(rows)
             wall, rng, ker = [], [], []
             for _ in range(args.reps):
-                torch.cuda.synchronize()
+                rtamd.device_synchronize()
                 t0 = time.perf_counter()
                 run(rows)
-                torch.cuda.synchronize()
+                rtamd.device_synchronize()
                 wall.append((time.perf_counter() - t0) * 1e3)
                 rng.append(st.ms_rng)
                 ker.append(st.ms_kernel)
@@ -95,15 +96,22 @@ def main():
         m = max(p["rows"] for p in per)
         bpp = 3 if args.rgb8 else 24
         last_chunk = (m - (args.chunks - 1) * m // args.chunks) * W * bpp
-        src = torch.empty(max(1, last_chunk * N), dtype=torch.uint8, device="cuda")
-        dst = torch.empty_like(src)
-        dst.copy_(src)
-        torch.cuda.synchronize()
+        # placement of the gathered slots on the root: the same row-scatter the
+        # product runs (k_scatter_rows / k_place_rows), timed on N * last-chunk rows
+        n_slots = max(1, (last_chunk // row_bytes) * N) if not args.rgb8 else max(1, (last_chunk * 8 // row_bytes) * N)
+        src = rtamd.DeviceBuffer(n_slots * row_bytes)
+        rows_d = rtamd.DeviceBuffer(n_slots * 4)
+        rows_d.from_host(np.arange(n_slots, dtype=np.int32) % H)
+        dst = rtamd.DeviceBuffer(H * row_bytes)
+        lib.rt_scatter_rows_device(src.ptr, rows_d.ptr, n_slots, W, dst.ptr, None)
+        rtamd.device_synchronize()
         tc = time.perf_counter()
         for _ in range(5):
-            dst.copy_(src)
-        torch.cuda.synchronize()
+            lib.rt_scatter_rows_device(src.ptr, rows_d.ptr, n_slots, W, dst.ptr, None)
+        rtamd.device_synchronize()
         place_ms = (time.perf_counter() - tc) / 5 * 1e3 if N > 1 else 0.0
+        if args.rgb8:
+            place_ms /= 8.0   # (3 B/px placed, the scatter above moved 24 B/px)
         g64 = (last_chunk / 64e9 * 1e3 + place_ms) if N > 1 else 0.0
         g153 = (last_chunk / 153e9 * 1e3 + place_ms) if N > 1 else 0.0
         out = {"config": args.config, "world": N, "strip": args.strip, "chunks": args.chunks, "two_streams": args.two_streams, "max_rank_wall_ms": round(worst, 3),
