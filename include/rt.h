@@ -238,7 +238,7 @@ int rt_render(const rt_scene* s, int W, int H, int mode, int flags,
 
 /* Tracer::render over n_gpus HIP devices of THIS process (n_gpus <= 0: all
  * visible devices): every device renders interleaved strips of RT_STRIP_ROWS
- * output rows (strip s -> device s mod n, rt_dist_rows), and the strips reach
+ * (paper mode: RT_PAPER_STRIP_ROWS) output rows (strip s -> device s mod n, rt_dist_rows), and the strips reach
  * device 0 through RCCL ncclGather over xGMI (one collective per row chunk,
  * overlapped with the tracing of the next chunk) before the one D2H copy into
  * fb_host.  The result is bit-identical to rt_render (same kernels, same
@@ -262,7 +262,8 @@ int rt_render_rgb8(const rt_scene* s, int W, int H, int mode, int flags, int n_g
  * (the ncclGather of rt_render_multi).  Non-root ranks pass NULL.  The call
  * returns when this rank's part (and on rank 0 the whole frame) is done;
  * stats are this rank's (ray counts of its rows). */
-#define RT_STRIP_ROWS 8
+#define RT_STRIP_ROWS 8          /* standard mode */
+#define RT_PAPER_STRIP_ROWS 30   /* paper mode: + 2 neighbour rows per strip = 32, four 8-row waves */
 #define RT_DIST_ID_BYTES 128
 typedef struct rt_dist rt_dist;
 int rt_dist_get_id(uint8_t id[RT_DIST_ID_BYTES]);
@@ -280,8 +281,11 @@ int rt_render_dist_rgb8(rt_dist* d, const rt_scene* s, int W, int H, int mode, i
 int rt_dist_reduce_max(rt_dist* d, double* vals_host, int n);
 int rt_dist_barrier(rt_dist* d);
 /* The partition: writes the output rows of `rank` (ascending) to rows_out
- * (room for H entries) and returns their count; <0 on bad arguments. */
+ * (room for H entries) and returns their count; <0 on bad arguments.
+ * rt_dist_rows is the standard-mode partition (RT_STRIP_ROWS); paper mode
+ * uses RT_PAPER_STRIP_ROWS strips (rt_dist_rows_mode). */
 int rt_dist_rows(int H, int world, int rank, int32_t* rows_out);
+int rt_dist_rows_mode(int H, int world, int rank, int mode, int32_t* rows_out);
 
 /* Render an arbitrary set of OUTPUT rows (top-row-first indices) into a
  * compact device buffer fb_rows_dev[n_rows][W][3] on the given HIP stream

@@ -1,8 +1,9 @@
 // rt_dist.hip — frames on several GPUs and the device output path.
 //
 // pixels are independent, so a frame is partitioned by OUTPUT
-// ROWS: strip s of RT_STRIP_ROWS rows goes to rank s mod N (interleaving
-// balances cheap sky rows against expensive geometry rows).  Every rank runs
+// ROWS: strip s of RT_STRIP_ROWS rows (paper mode: RT_PAPER_STRIP_ROWS) goes
+// to rank s mod N (interleaving balances cheap sky rows against expensive
+// geometry rows).  Every rank runs
 // the ordinary trace (rt_frame_* of rt_render.hip) on its rows, chunk by
 // chunk, and each chunk is handed to ONE RCCL collective, ncclGather to rank
 // 0 over xGMI, on a high-priority stream so it overlaps the tracing of the
@@ -80,25 +81,38 @@ struct DevBuf {
 };
 
 // ------------------------------------------------------------- partition
-std::vector<int32_t> strip_rows(int H, int world, int rank) {
+// Strip height per mode: standard mode RT_STRIP_ROWS (8); paper mode
+// RT_PAPER_STRIP_ROWS (30): each strip's primary hits are traced with its two
+// neighbour rows (the edge probes, tracer.cpp:133-178), and 30 + 2 = 32 rows
+// keep every 8-row wave of k_paper_primary inside one strip (coherent rays
+// for the wave-level culls) at 1/15 halo overhead (8-row strips: 1/4 extra
+// rows and waves straddling strips 16+ rows apart).
+int strip_height(int mode) { return mode == RT_MODE_PAPER ? RT_PAPER_STRIP_ROWS : RT_STRIP_ROWS; }
+
+std::vector<int32_t> strip_rows(int H, int world, int rank, int S = RT_STRIP_ROWS) {
     std::vector<int32_t> rows;
-    for (int s = 0; s * RT_STRIP_ROWS < H; ++s)
+    for (int s = 0; s * S < H; ++s)
         if (s % world == rank)
-            for (int r = s * RT_STRIP_ROWS; r < std::min(H, (s + 1) * RT_STRIP_ROWS); ++r) rows.push_back(r);
+            for (int r = s * S; r < std::min(H, (s + 1) * S); ++r) rows.push_back(r);
     return rows;
 }
 
-int max_rows(int H, int world) {
+int max_rows(int H, int world, int S = RT_STRIP_ROWS) {
     int m = 0;
-    for (int r = 0; r < world; ++r) m = std::max(m, (int)strip_rows(H, world, r).size());
+    for (int r = 0; r < world; ++r) m = std::max(m, (int)strip_rows(H, world, r, S).size());
     return m;
 }
 
-std::vector<std::pair<int, int>> chunk_bounds(int m, int chunks) {
-    chunks = std::max(1, std::min(chunks, m));
+// `chunks` contiguous pieces of [0, m), each a whole number of strips of S
+// rows (a chunk never splits a strip, so a paper-mode strip's rows and halo
+// are traced by one launch).
+std::vector<std::pair<int, int>> chunk_bounds(int m, int chunks, int S = 1) {
+    const int units = (m + S - 1) / S;
+    chunks = std::max(1, std::min(chunks, units));
     std::vector<std::pair<int, int>> out;
     for (int k = 0; k < chunks; ++k) {
-        const int a = (int)((int64_t)k * m / chunks), b = (int)((int64_t)(k + 1) * m / chunks);
+        const int a = std::min(m, (int)((int64_t)k * units / chunks) * S);
+        const int b = std::min(m, (int)((int64_t)(k + 1) * units / chunks) * S);
         if (b > a) out.emplace_back(a, b);
     }
     if (out.empty()) out.emplace_back(0, 0);
@@ -188,13 +202,14 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     std::lock_guard<std::mutex> lk(D.mu);
     int rc = dist_init_streams(D);
     if (rc != RT_OK) return rc;
-    const std::vector<int32_t> rows = strip_rows(H, D.world, D.rank);
+    const int S = strip_height(mode);
+    const std::vector<int32_t> rows = strip_rows(H, D.world, D.rank, S);
     const int n = (int)rows.size();
-    const int m = max_rows(H, D.world);
+    const int m = max_rows(H, D.world, S);
     const size_t row_elems = (size_t)W * 3;
     const size_t row_bytes = row_elems * (kind ? 1 : sizeof(double));
     const bool coll = D.collective();
-    const auto bounds = chunk_bounds(m, coll ? kChunks : 1);
+    const auto bounds = chunk_bounds(m, coll ? kChunks : 1, S);
     const bool direct = !coll && kind == 0;   // trace straight into the caller's frame
     if (!direct) HIP_TRY(D.mine.ensure(std::max<size_t>(1, (size_t)m * row_elems * sizeof(double))));
     if (kind == 1 && coll) HIP_TRY(D.mine8.ensure(std::max<size_t>(1, (size_t)m * row_elems)));
@@ -204,7 +219,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         // placement table: chunk k occupies slots [world*a, world*b) as [rank][b-a]
         D.rowtab_host.assign((size_t)D.world * m, -1);
         for (int r = 0; r < D.world; ++r) {
-            const std::vector<int32_t> rr = strip_rows(H, D.world, r);
+            const std::vector<int32_t> rr = strip_rows(H, D.world, r, S);
             for (const auto& ab : bounds)
                 for (int i = ab.first; i < ab.second; ++i)
                     D.rowtab_host[(size_t)D.world * ab.first + (size_t)r * (ab.second - ab.first) + (i - ab.first)] =
@@ -471,11 +486,17 @@ int render_multi(const rt_scene* s, int W, int H, int mode, int flags, int n_gpu
 }  // namespace
 
 // ------------------------------------------------------------------ C-ABI
-extern "C" int rt_dist_rows(int H, int world, int rank, int32_t* rows_out) {
-    if (H <= 0 || world <= 0 || rank < 0 || rank >= world || !rows_out) return RT_ERR_INVALID_ARG;
-    const std::vector<int32_t> r = strip_rows(H, world, rank);
+extern "C" int rt_dist_rows_mode(int H, int world, int rank, int mode, int32_t* rows_out) {
+    if (H <= 0 || world <= 0 || rank < 0 || rank >= world || !rows_out ||
+        (mode != RT_MODE_STANDARD && mode != RT_MODE_PAPER))
+        return RT_ERR_INVALID_ARG;
+    const std::vector<int32_t> r = strip_rows(H, world, rank, strip_height(mode));
     std::copy(r.begin(), r.end(), rows_out);
     return (int)r.size();
+}
+
+extern "C" int rt_dist_rows(int H, int world, int rank, int32_t* rows_out) {
+    return rt_dist_rows_mode(H, world, rank, RT_MODE_STANDARD, rows_out);
 }
 
 extern "C" int rt_render_multi(const rt_scene* s, int W, int H, int mode, int flags, int n_gpus, double* fb_host,

@@ -163,12 +163,13 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool active = x < P.W && li < P.n_list;
+    // (list entries < 0 pad a run of consecutive rows to a wave boundary)
+    const int ei = li < P.n_list ? P.ext_list[li] : -1;
+    const bool active = x < P.W && ei >= 0;
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
     cnt.init();
     if (active) {
-        const int ei = P.ext_list[li];
         const int y = P.ext_rows[ei];
         const DRay r = gen_ray(S, x, y);
         real ht = RV(0.0);

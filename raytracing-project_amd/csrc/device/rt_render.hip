@@ -488,7 +488,9 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         ints.insert(ints.end(), ext_shade.begin(), ext_shade.end());
         ints.insert(ints.end(), nbr.begin(), nbr.end());
         ints.insert(ints.end(), f->rows.begin(), f->rows.end());
-        HIP_TRY(ws.paper_aux.ensure((ints.size() + f->n_ext) * sizeof(int32_t)));
+        // (+ the ext lists of the trace calls: every entry at most once, each
+        // run padded by < 8 to a wave boundary: <= 8 * n_ext entries)
+        HIP_TRY(ws.paper_aux.ensure((ints.size() + 8 * (size_t)f->n_ext) * sizeof(int32_t)));
         HIP_TRY(hipMemcpyAsync(ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
         const size_t npx = (size_t)f->n_ext * W;
         HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
@@ -530,8 +532,13 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         else rtd::launch_std(f->eager, f->deep, f->secondary, f->count_ops, st, f->S, P);
         HIP_TRY(hipGetLastError());
     } else {
-        // primary hits of the ext rows this chunk reads that no earlier chunk computed
+        // primary hits of the ext rows this chunk reads that no earlier chunk
+        // computed.  k_paper_primary's waves are 8 list entries tall: each run
+        // of consecutive rows starts on a wave boundary (entries -1 pad), so no
+        // wave mixes rows of different strips (the wave-level culls need
+        // coherent rays).
         std::vector<int32_t> list;
+        int prev_row = -2;
         for (int i = ri0; i < ri1; ++i) {
             const int r = f->rows[i];
             for (int rr = r - 1; rr <= r + 1; ++rr) {
@@ -539,7 +546,10 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
                 const int e = f->ext_pos[rr];
                 if (e >= 0 && !f->ext_done[e]) {
                     f->ext_done[e] = 1;
+                    if (rr != prev_row + 1)
+                        while (list.size() % 8) list.push_back(-1);
                     list.push_back(e);
+                    prev_row = rr;
                 }
             }
         }
@@ -569,6 +579,10 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         P.fb = fb;
         P.counters = ctr;
         if (!list.empty()) {
+            if ((size_t)f->list_used + list.size() > 8 * (size_t)n_ext) {
+                rtamd::set_last_error("rt_frame_trace: paper-mode list overflow");
+                return RT_ERR_PROCESSING;
+            }
             f->list_used += (int)list.size();
             f->stage.push_back(std::move(list));
             const std::vector<int32_t>& L = f->stage.back();

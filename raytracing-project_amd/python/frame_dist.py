@@ -8,7 +8,12 @@ Used by bench.py (RCCL, device buffers) and tests/test_dist_gloo.py (gloo).
 """
 from __future__ import annotations
 
-STRIP = 8
+STRIP = 8          # RT_STRIP_ROWS (standard mode)
+PAPER_STRIP = 30   # RT_PAPER_STRIP_ROWS (paper mode: + 2 neighbour rows = four 8-row waves)
+
+
+def strip_for(mode: int) -> int:
+    return PAPER_STRIP if mode == 1 else STRIP
 
 
 def strip_rows(H: int, rank: int, world: int, strip: int = STRIP) -> list[int]:
@@ -33,11 +38,13 @@ def gather_row_index(H: int, world: int, strip: int = STRIP) -> list[int]:
     return out
 
 
-def chunk_bounds(m: int, chunks: int) -> list[tuple[int, int]]:
+def chunk_bounds(m: int, chunks: int, strip: int = 1) -> list[tuple[int, int]]:
     """Split the padded per-rank row list [0, m) into `chunks` contiguous
-    pieces (the pipeline units: chunk k is gathered while k+1 is traced)."""
-    chunks = max(1, min(chunks, m)) if m > 0 else 1
-    out = [(k * m // chunks, (k + 1) * m // chunks) for k in range(chunks)]
+    pieces of whole strips (the pipeline units: chunk k is gathered while k+1
+    is traced; rt_dist.hip chunk_bounds)."""
+    units = (m + strip - 1) // strip if m > 0 else 0
+    chunks = max(1, min(chunks, units)) if units > 0 else 1
+    out = [(min(m, k * units // chunks * strip), min(m, (k + 1) * units // chunks * strip)) for k in range(chunks)]
     return [(a, b) for a, b in out if b > a] or [(0, 0)]
 
 
@@ -61,7 +68,7 @@ class DistFrame:
         self.W, self.H, self.rank, self.world = W, H, rank, world
         self.rows = strip_rows(H, rank, world, strip)
         self.m = max_rows(H, world, strip)
-        self.bounds = chunk_bounds(self.m, chunks if world > 1 else 1)
+        self.bounds = chunk_bounds(self.m, chunks if world > 1 else 1, strip)
         self.mine = torch.zeros((self.m, W, 3), dtype=torch.float64, device=device)
         self.stage = self.full = self.slot_rows = None
         if world > 1 and rank == 0:

@@ -174,6 +174,7 @@ def amd_lib():
         lib.rt_render_dist_rgb8.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_void_p, C.POINTER(Stats)]
         lib.rt_dist_rows.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32)]
+        lib.rt_dist_rows_mode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32)]
         lib.rt_test_render_dist_sim.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                 _dp, C.POINTER(C.c_uint8)]
         lib.rt_dist_reduce_max.argtypes = [C.c_void_p, _dp, C.c_int]
@@ -480,10 +481,11 @@ def render_rgb8(scene: Scene, width: int, height: int, mode: int, n_gpus: int = 
     return out
 
 
-def dist_rows(H: int, world: int, rank: int) -> list[int]:
-    """rt_dist_rows: the output rows rank renders (interleaved strips)."""
+def dist_rows(H: int, world: int, rank: int, mode: int = RT_MODE_STANDARD) -> list[int]:
+    """rt_dist_rows_mode: the output rows rank renders (interleaved strips of
+    RT_STRIP_ROWS, paper mode RT_PAPER_STRIP_ROWS)."""
     buf = (C.c_int32 * max(1, H))()
-    n = amd_lib().rt_dist_rows(H, world, rank, buf)
+    n = amd_lib().rt_dist_rows_mode(H, world, rank, mode, buf)
     if n < 0:
         raise RTError(n, "rt_dist_rows: bad arguments")
     return list(buf[:n])

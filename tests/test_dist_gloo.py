@@ -45,7 +45,7 @@ def _worker(rank, world, port, text, mode, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
-    df = frame_dist.DistFrame(W, H, rank, world, "cpu", chunks=3)
+    df = frame_dist.DistFrame(W, H, rank, world, "cpu", chunks=3, strip=frame_dist.strip_for(mode))
 
     def trace_chunk(a, b, out, stream):   # row by row: arbitrary stream offsets
         for k in range(a, b):
@@ -96,9 +96,11 @@ def test_strip_partition_covers_frame():
             assert sorted(r for r in idx if r >= 0) == list(range(H))
             m = frame_dist.max_rows(H, world)
             for chunks in (1, 3, 4, 64):
-                b = frame_dist.chunk_bounds(m, chunks)
-                assert b[0][0] == 0 and b[-1][1] == m
-                assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+                for strip in (1, 8, 30):
+                    b = frame_dist.chunk_bounds(m, chunks, strip)
+                    assert b[0][0] == 0 and b[-1][1] == m
+                    assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+                    assert all(a % strip == 0 for a, _ in b)   # chunks never split a strip
 
 
 def _rdv_worker(rank, tag, out):

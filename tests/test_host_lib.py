@@ -35,18 +35,22 @@ def test_libraries_export_every_declared_symbol():
     assert amd.rt_abi_version() == 4
 
 
-@pytest.mark.parametrize("H,world", [(2160, 8), (2160, 3), (1080, 2), (17, 4), (5, 8), (1, 1)])
-def test_dist_partition(rt, H, world):
-    """rt_dist_rows: interleaved RT_STRIP_ROWS strips, every
-    output row on exactly one rank, ascending per rank, balanced to a strip."""
-    rows = [rt.dist_rows(H, world, r) for r in range(world)]
+@pytest.mark.parametrize("H,world", [(2160, 8), (2160, 3), (1080, 2), (17, 4), (5, 8), (1, 1), (4320, 8)])
+@pytest.mark.parametrize("mode,S", [(0, 8), (1, 30)])
+def test_dist_partition(rt, H, world, mode, S):
+    """rt_dist_rows_mode: interleaved strips of RT_STRIP_ROWS
+    (paper mode RT_PAPER_STRIP_ROWS), every output row on exactly one rank,
+    ascending per rank, balanced to a strip."""
+    rows = [rt.dist_rows(H, world, r, mode) for r in range(world)]
     flat = sorted(x for rr in rows for x in rr)
     assert flat == list(range(H))
     for r, rr in enumerate(rows):
         assert rr == sorted(rr)
-        assert all((x // 8) % world == r for x in rr)
+        assert all((x // S) % world == r for x in rr)
     sizes = [len(rr) for rr in rows]
-    assert max(sizes) - min(sizes) <= 8
+    assert max(sizes) - min(sizes) <= S
+    if mode == 0:
+        assert rows == [rt.dist_rows(H, world, r) for r in range(world)]   # rt_dist_rows = standard
 
 
 def test_dist_partition_matches_python_mirror(rt):

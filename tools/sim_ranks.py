@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--strip", type=int, default=frame_dist.STRIP)
+    ap.add_argument("--strip", type=int, default=None, help="strip height (default: the product's for the mode)")
     ap.add_argument("--chunks", type=int, default=4, help="trace through rt_frame_* in this many chunks")
     ap.add_argument("--rgb8", action="store_true", help="gather 3 B/px (the CLI path) instead of FP64")
     ap.add_argument("--one-stream", dest="two_streams", action="store_false",
@@ -48,6 +48,7 @@ def main():
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
+    strip = args.strip or frame_dist.strip_for(mode)
     lib = rtamd.amd_lib()
     row_bytes = W * 3 * 8
     buf = rtamd.DeviceBuffer(H * row_bytes)
@@ -65,7 +66,7 @@ def main():
         rc = lib.rt_frame_begin(sc.handle, W, H, mode, 0, (C.c_int32 * len(rows))(*rows), len(rows),
                                 stream.handle, C.byref(fr))
         assert rc == 0, rtamd.last_error()
-        for k, (a, b) in enumerate(frame_dist.chunk_bounds(len(rows), args.chunks)):
+        for k, (a, b) in enumerate(frame_dist.chunk_bounds(len(rows), args.chunks, strip)):
             s = streams[k % len(streams)]
             rc = lib.rt_frame_trace(fr, a, b, C.c_void_p(buf.ptr.value + a * row_bytes), s.handle)
             assert rc == 0, rtamd.last_error()
@@ -76,7 +77,7 @@ def main():
     for N in [int(v) for v in args.worlds.split(",")]:
         per = []
         for r in range(N):
-            rows = rtamd.dist_rows(H, N, r) if args.strip == frame_dist.STRIP else frame_dist.strip_rows(H, r, N, args.strip)
+            rows = rtamd.dist_rows(H, N, r, mode) if args.strip is None else frame_dist.strip_rows(H, r, N, args.strip)
             run(rows)
             wall, rng, ker = [], [], []
             for _ in range(args.reps):
@@ -114,7 +115,7 @@ def main():
             place_ms /= 8.0   # (3 B/px placed, the scatter above moved 24 B/px)
         g64 = (last_chunk / 64e9 * 1e3 + place_ms) if N > 1 else 0.0
         g153 = (last_chunk / 153e9 * 1e3 + place_ms) if N > 1 else 0.0
-        out = {"config": args.config, "world": N, "strip": args.strip, "chunks": args.chunks, "two_streams": args.two_streams, "max_rank_wall_ms": round(worst, 3),
+        out = {"config": args.config, "world": N, "strip": strip, "chunks": args.chunks, "two_streams": args.two_streams, "max_rank_wall_ms": round(worst, 3),
                "max_rank_rng_ms": round(max(p["rng_ms"] for p in per), 3),
                "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
                "min_rank_kernel_ms": round(min(p["kernel_ms"] for p in per), 3),
