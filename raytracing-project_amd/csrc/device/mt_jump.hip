@@ -80,6 +80,7 @@ __device__ __forceinline__ int ckpt_parts(int64_t c, const int8_t* parts) {
 }
 
 struct JumpArgs {
+    int64_t div;                // partial-window slot of checkpoint c: c / div (1, or R for the coarse table tree)
     int64_t lo;                 // R^j: this level computes checkpoints in [lo, R*lo)
     const int64_t* list;        // the checkpoints of this level to compute (gridDim.x of them)
     int S;                      // partial jumps per checkpoint (gridDim.y)
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint16_t* __rest
     const int np = ckpt_parts(r, A.parts);
     for (int k = tid; k < N; k += blockDim.x) {
         uint32_t v = 0;
-        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)r * rtamd::kMTParts + p) * N + k];
+        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)(r / A.div) * rtamd::kMTParts + p) * N + k];
         buf[k] = v;
     }
     const int n_all = A.len[m];
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(JUMP_THREADS) void k_mt_jump(const uint16_t* __rest
             a0 ^= sa[tp[i]];
             b0 ^= sb[tp[i]];
         }
-        uint32_t* out = ckpt + ((size_t)c * rtamd::kMTParts + s) * N;
+        uint32_t* out = ckpt + ((size_t)(c / A.div) * rtamd::kMTParts + s) * N;
         out[tid] = a0 ^ a1;
         out[tid + N / 2] = b0 ^ b1;
     }
@@ -259,16 +260,45 @@ inline int64_t ckpt_parent(int64_t c) {
     return c - (c / lo) * lo;
 }
 
-// Consolidate the partial windows of checkpoints [c0, c1) into the table.
-__global__ void k_mt_consolidate(const uint32_t* __restrict__ ckpt, JumpArgs A, int64_t c0, int64_t c1,
-                                 uint32_t* __restrict__ table) {
-    const int64_t c = c0 + blockIdx.x;
-    if (c >= c1) return;
-    const int np = ckpt_parts(c, A.parts);
-    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+// Table expansion: ONE wavefront per coarse checkpoint c' (window at table
+// entry R*c', from the jump tree's partial windows) walks the stream forward
+// sequentially and stores the window at every kTableK-th block, i.e. table
+// entries R*c' .. R*c' + R-1 (< n).  Sequential twisting of R*kTableK blocks
+// per wave replaces R-1 GF(2) jumps of ~10^4 taps each.
+__global__ __launch_bounds__(64) void k_mt_expand(const uint32_t* __restrict__ ckpt, JumpArgs A, int64_t n,
+                                                  uint32_t* __restrict__ table) {
+    __shared__ uint32_t buf[2 * N];
+    const int lane = threadIdx.x;
+    const int64_t cc = blockIdx.x;               // coarse slot
+    const int64_t c0 = cc * rtamd::kMTRadix;     // its table entry
+    const int np = ckpt_parts(c0, A.parts);
+    for (int k = lane; k < N; k += 64) {
         uint32_t v = 0;
-        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)c * rtamd::kMTParts + p) * N + k];
-        table[(size_t)c * N + k] = v;
+        for (int p = 0; p < np; ++p) v ^= ckpt[((size_t)cc * rtamd::kMTParts + p) * N + k];
+        buf[k] = v;
+    }
+    lds_barrier();
+    int base = 0;
+    for (int e = 0; e < rtamd::kMTRadix && c0 + e < n; ++e) {
+        uint32_t* dst = table + (size_t)(c0 + e) * N;
+        for (int k = lane; k < N; k += 64) dst[k] = buf[base + k];
+        if (e + 1 == rtamd::kMTRadix || c0 + e + 1 >= n) break;
+        for (int b = 0; b < rtamd::kTableK; ++b) {   // advance one segment
+            const uint32_t* o = buf + base;
+            uint32_t* nw = buf + (base ^ N);
+            for (int t = lane; t < 227; t += 64) {
+                const uint32_t n0 = twist_word(o[t], o[t + 1], o[t + 397]);
+                const uint32_t n1 = twist_word(o[227 + t], o[228 + t], n0);
+                nw[t] = n0;
+                nw[227 + t] = n1;
+                if (t < 170) {
+                    const uint32_t nx = (t == 169) ? twist_word(o[0], o[1], o[397]) : o[455 + t];
+                    nw[454 + t] = twist_word(o[454 + t], nx, n1);
+                }
+            }
+            lds_barrier();
+            base ^= N;
+        }
     }
 }
 
@@ -368,20 +398,25 @@ hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
         e = plan.build(kTableK, levels);
         if (e != hipSuccess) return e;
     }
-    // every checkpoint of [0, n_new) by the radix-64 jump tree into partial
-    // windows, then consolidated into a new table
+    // The coarse checkpoints (every R-th table entry: c = R*c') by the jump
+    // tree's levels >= 1 (each from a coarse parent, c mod R^j), as partial
+    // windows in slot c' of d_ckpt; then one wave per coarse checkpoint fills
+    // the R entries behind it by sequential twisting (k_mt_expand).
+    const int64_t R = rtamd::kMTRadix;
+    const int64_t n_coarse = (n_new + R - 1) / R;
     std::vector<int64_t> lists;
     int64_t lvl_off[MAX_LEVELS + 1] = {0};
     for (int j = 0; j < plan.levels; ++j) {
         const int64_t lo = (int64_t)1 << (kMTRadixBits * j);
-        for (int64_t c = lo; c < std::min(n_new, lo * kMTRadix); ++c) lists.push_back(c);
+        if (j >= 1)
+            for (int64_t c = lo; c < std::min(n_coarse * R, lo * R); c += R) lists.push_back(c);
         lvl_off[j + 1] = (int64_t)lists.size();
     }
     uint32_t* d_ckpt = nullptr;
     int64_t* d_list = nullptr;
     uint32_t* d_tab = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    e = hipMalloc(&d_ckpt, (size_t)n_new * kMTParts * N * sizeof(uint32_t));
+    e = hipMalloc(&d_ckpt, (size_t)n_coarse * kMTParts * N * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&d_list, std::max<size_t>(1, lists.size()) * sizeof(int64_t));
     if (e == hipSuccess) e = hipMalloc(&d_tab, (size_t)n_new * N * sizeof(uint32_t));
     if (e == hipSuccess) e = hipEventCreate(&e0);
@@ -396,8 +431,9 @@ hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
         if (n_j > 0) parts[j] = (int8_t)level_parts(n_j);
     }
     JumpArgs A{};
+    A.div = R;
     for (int k = 0; k < MAX_LEVELS; ++k) A.parts[k] = parts[k];
-    for (int j = 0; j < plan.levels && e == hipSuccess; ++j) {
+    for (int j = 1; j < plan.levels && e == hipSuccess; ++j) {
         const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
         if (n_j <= 0) continue;
         A.lo = (int64_t)1 << (kMTRadixBits * j);
@@ -412,8 +448,7 @@ hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mt_consolidate, dim3((unsigned)n_new), dim3(256), 0, stream, d_ckpt, A, (int64_t)0,
-                           n_new, d_tab);
+        hipLaunchKernelGGL(k_mt_expand, dim3((unsigned)n_coarse), dim3(64), 0, stream, d_ckpt, A, n_new, d_tab);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipEventRecord(e1, stream);
@@ -602,6 +637,7 @@ hipError_t mt_launch_jitter(const JitterPlan& plan, const std::vector<JRange>& r
         const int64_t n_j = lvl_off[j + 1] - lvl_off[j];
         if (n_j <= 0) continue;
         JumpArgs A;
+        A.div = 1;
         A.lo = (int64_t)1 << (kMTRadixBits * j);
         A.list = dL + lvl_off[j];
         A.S = parts[j];

@@ -105,14 +105,20 @@ int max_rows(int H, int world, int S = RT_STRIP_ROWS) {
 
 // `chunks` contiguous pieces of [0, m), each a whole number of strips of S
 // rows (a chunk never splits a strip, so a paper-mode strip's rows and halo
-// are traced by one launch).
+// are traced by one launch), of decreasing size: weights chunks, chunks-1,
+// ..., 1 (4 chunks: 40/30/20/10 %).  Chunk k is gathered while chunk k+1 is
+// traced, so only the last, smallest chunk's gather is exposed.
 std::vector<std::pair<int, int>> chunk_bounds(int m, int chunks, int S = 1) {
-    const int units = (m + S - 1) / S;
-    chunks = std::max(1, std::min(chunks, units));
+    const int64_t units = (m + S - 1) / S;
+    chunks = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, units));
+    const int64_t wsum = (int64_t)chunks * (chunks + 1) / 2;
     std::vector<std::pair<int, int>> out;
+    int64_t acc = 0;
     for (int k = 0; k < chunks; ++k) {
-        const int a = std::min(m, (int)((int64_t)k * units / chunks) * S);
-        const int b = std::min(m, (int)((int64_t)(k + 1) * units / chunks) * S);
+        const int64_t u0 = acc * units / wsum;
+        acc += chunks - k;
+        const int64_t u1 = acc * units / wsum;
+        const int a = (int)std::min<int64_t>(m, u0 * S), b = (int)std::min<int64_t>(m, u1 * S);
         if (b > a) out.emplace_back(a, b);
     }
     if (out.empty()) out.emplace_back(0, 0);

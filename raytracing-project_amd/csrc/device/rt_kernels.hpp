@@ -169,29 +169,40 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
     cnt.init();
+    DRay r{v3(RV(0.0), RV(0.0), RV(0.0)), v3(RV(0.0), RV(0.0), -RV(1.0))};
+    real ht = RV(0.0);
+    DHit h;
+    h.mat = -1;
+    h.p = h.n = v3(RV(0.0), RV(0.0), RV(0.0));
+    h.ff = 1;
+    bool hits = false, sh = false;
+    size_t idx = 0;
     if (active) {
         const int y = P.ext_rows[ei];
-        const DRay r = gen_ray(S, x, y);
-        real ht = RV(0.0);
-        DHit h;
+        r = gen_ray(S, x, y);
         ++ni;
-        h.mat = -1;
-        bool hits;
         if constexpr (WV)
             hits = scene_intersect_wave<E, D>(S, r, RV(1e-4), RT_INF, ht, h, __builtin_amdgcn_read_exec() == ~0ull,
                                               cnt);
         else
             hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
-        const size_t idx = (size_t)ei * P.W + x;
+        idx = (size_t)ei * P.W + x;
         P.hit[idx] = hits ? 1 : 0;
         P.t[idx] = ht;
         P.nx[idx] = h.n.x;
         P.ny[idx] = h.n.y;
         P.nz[idx] = h.n.z;
         P.mat[idx] = hits ? h.mat : -3;
-        if (P.ext_shade[ei]) {
-            // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125)
-            V3 base = shade<E, D, DL, WV, true>(S, ht, h, normalized(vneg(r.d)), no, cnt, hits);
+        sh = P.ext_shade[ei] != 0;   // (a neighbour-only row needs the hit, not the shading)
+    }
+    // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125).  shade()
+    // runs with the whole wave (lanes with nothing to shade pass valid =
+    // false) so that the wave-level shadow culls keep a full wave even when
+    // it mixes shaded rows and neighbour-only rows (strip edges of a
+    // multi-GPU partition) or inactive lanes.
+    if (__any(sh)) {
+        V3 base = shade<E, D, DL, WV, true>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
+        if (sh) {
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             P.lum[idx] = RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z;
         }

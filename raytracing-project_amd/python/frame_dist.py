@@ -40,11 +40,18 @@ def gather_row_index(H: int, world: int, strip: int = STRIP) -> list[int]:
 
 def chunk_bounds(m: int, chunks: int, strip: int = 1) -> list[tuple[int, int]]:
     """Split the padded per-rank row list [0, m) into `chunks` contiguous
-    pieces of whole strips (the pipeline units: chunk k is gathered while k+1
-    is traced; rt_dist.hip chunk_bounds)."""
+    pieces of whole strips, of decreasing size (the pipeline units: chunk k is
+    gathered while k+1 is traced, so only the smallest, last one's gather is
+    exposed; rt_dist.hip chunk_bounds)."""
     units = (m + strip - 1) // strip if m > 0 else 0
     chunks = max(1, min(chunks, units)) if units > 0 else 1
-    out = [(min(m, k * units // chunks * strip), min(m, (k + 1) * units // chunks * strip)) for k in range(chunks)]
+    wsum = chunks * (chunks + 1) // 2   # decreasing sizes: weights chunks, chunks-1, ..., 1
+    out, acc = [], 0
+    for k in range(chunks):
+        u0 = acc * units // wsum
+        acc += chunks - k
+        u1 = acc * units // wsum
+        out.append((min(m, u0 * strip), min(m, u1 * strip)))
     return [(a, b) for a, b in out if b > a] or [(0, 0)]
 
 

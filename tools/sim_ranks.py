@@ -7,8 +7,9 @@ rt_frame_* in the product's 4 row chunks and timed (host wall clock around
 the blocking call, plus the library's HIP-event split into jitter stream and
 trace kernel).  The slowest rank bounds the N-GPU step before the gather.
 
-The gather is added as a model: chunks 1..3 of a rank are gathered while the
-next chunk traces, so the exposed part is the LAST chunk's ncclGather into
+The gather is added as a model: chunks 1..3 of a rank (40/30/20/10 % of its
+rows) are gathered while the next chunk traces, so the exposed part is the
+LAST (smallest) chunk's ncclGather into
 rank 0 (N-1 peers, each on its own xGMI link, in parallel) plus its
 placement on the root; a link is priced at 64 GB/s (conservative) and 153
 GB/s (the per-link figure of the MI355X spec sheet), the placement at the
@@ -96,7 +97,8 @@ def main():
         # exposed gather of the last chunk (model) + its placement on the root (measured copy rate)
         m = max(p["rows"] for p in per)
         bpp = 3 if args.rgb8 else 24
-        last_chunk = (m - (args.chunks - 1) * m // args.chunks) * W * bpp
+        a_last, b_last = frame_dist.chunk_bounds(m, args.chunks, strip)[-1]   # the product's (decreasing) chunks
+        last_chunk = (b_last - a_last) * W * bpp
         # placement of the gathered slots on the root: the same row-scatter the
         # product runs (k_scatter_rows / k_place_rows), timed on N * last-chunk rows
         n_slots = max(1, (last_chunk // row_bytes) * N) if not args.rgb8 else max(1, (last_chunk * 8 // row_bytes) * N)
