@@ -1503,10 +1503,9 @@ __device__ __forceinline__ bool line_touch(const float* g, float ox, float oy, f
     const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
     const float R = g[3] + rho + m;
     const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
-    if (!(L2 > R * R)) return true;
     const float wa = __builtin_fabsf(__builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az)));
     const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
-    return !(wa + m < rhs);
+    return !(L2 > R * R) | !(wa + m < rhs);   // (no branch: lanes disagree on the first test)
 }
 
 template <class CT>
@@ -1519,18 +1518,20 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
 __device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, float ax, float ay, float az, float bx,
                                              float by, float bz, float ux, float uy, float uz, float uu, float rho,
                                              float mag) {
+    // Lanes test objects of different types side by side, so both tests run
+    // on every lane and the type selects (no divergent branches, no exec
+    // bookkeeping between the record's loads and the ballot).
     const int type = __float_as_int(c1.x);
-    if (type == 3) {
-        // a bare half-space: the segments cross its plane only if the capsule
-        // does (both axis ends farther than rho on one side: no lane); n.x - n.p
-        // in f32 is within 1e-6 of the magnitudes of the signed distance, far
-        // inside the margin
-        const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
-        const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
-        const float m = rho + 1e-5f * (mag + c1.y);
-        return !((sa > m && sb > m) || (sa < -m && sb < -m));   // NaN passes
-    }
-    return type == 1 || (type == 2 && capsule_touch(c0, ax, ay, az, ux, uy, uz, uu, rho, mag));
+    // a bare half-space: the segments cross its plane only if the capsule
+    // does (both axis ends farther than rho on one side: no lane); n.x - n.p
+    // in f32 is within 1e-6 of the magnitudes of the signed distance, far
+    // inside the margin
+    const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
+    const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
+    const float m = rho + 1e-5f * (mag + c1.y);
+    const bool plane = !((sa > m) & (sb > m)) & !((sa < -m) & (sb < -m));   // NaN passes
+    const bool ball = capsule_touch(c0, ax, ay, az, ux, uy, uz, uu, rho, mag);
+    return (type == 1) | ((type == 2) & ball) | ((type == 3) & plane);
 }
 
 // Scene::occluded for the querying lanes of a fully active wave.  Returns
@@ -1585,13 +1586,13 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
     for (int base = 0; base < S.n_objs; base += 64) {
         const int nc = S.n_objs - base;
         const int j = base + lane;
-        bool pass = false;
-        if (j < S.n_objs) {
-            // the object's cull record (CompiledScene::ctab): one 32-byte load
-            const float4 c0 = S.ctab[2 * j], c1 = S.ctab[2 * j + 1];
-            pass = cap ? record_touch(c0, c1, ax, ay, az, bx, by, bz, ux, uy, uz, uu, rho, mag)
-                       : __float_as_int(c1.x) != 0;
-        }
+        // the object's cull record (CompiledScene::ctab): one 32-byte load on
+        // every lane (lanes past the last object re-read it and are masked)
+        const int jr = j < S.n_objs ? j : S.n_objs - 1;
+        const float4 c0 = S.ctab[2 * jr], c1 = S.ctab[2 * jr + 1];
+        const bool pass = (j < S.n_objs) &
+                          (cap ? record_touch(c0, c1, ax, ay, az, bx, by, bz, ux, uy, uz, uu, rho, mag)
+                               : __float_as_int(c1.x) != 0);
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
         uint64_t m = (cap && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
@@ -1713,31 +1714,44 @@ __device__ __forceinline__ bool cone_touch(const float4 g, float ox, float oy, f
     const float m = 1e-5f * (mag + __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w);
     const float R = g.w + rho + m;
     const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
-    if (!(L2 > R * R)) return true;   // the bundle's origin region touches the ball (or NaN)
     const float wa = __builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az));
-    // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R
+    // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R;
+    // !(L2 > R^2): the bundle's origin region touches the ball (or NaN).  No
+    // branch: lanes disagree on the first test.
     const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
-    return !(wa + m < rhs);
+    return !(L2 > R * R) | !(wa + m < rhs);
 }
 __device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
                                           float az, float cth, float sth, float rho, float mag) {
     return cone_touch(*reinterpret_cast<const float4*>(g), ox, oy, oz, ax, ay, az, cth, sth, rho, mag);
 }
 
+//
+// valid = false: a lane that only keeps the wave fully active (trace_wave's
+// finished paths); its ray is left out of the bundle and of every test, its
+// result is garbage and its ops are not counted.
 template <bool EAGER, bool DEEP, class CT>
 __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin, real tmax, real& t_best,
-                                     DHit& best, bool wave_ok, CT& cnt) {
+                                     DHit& best, bool wave_ok, CT& cnt, bool valid = true) {
     cnt.pb(PH_WAVE_SETUP);
+    const uint64_t vm = __ballot(valid);
+    if (!vm) {
+        cnt.pe(PH_WAVE_SETUP);
+        return false;
+    }
+    const int f = __builtin_ctzll(vm);   // the bundle's axis lane
     const FRay fr = to_fray(r);
     const bool fin = __builtin_isfinite(fr.ox + fr.oy + fr.oz + fr.dx + fr.dy + fr.dz);
     // no cone for a partially active wave or non-finite rays: every object is
     // a candidate (the per-lane ball test still runs)
-    const bool cone = S.cull && wave_ok && exec_full() && !__any(!fin) && tmin >= RV(0.0);
-    const float ox = rdlane_f(fr.ox, 0), oy = rdlane_f(fr.oy, 0), oz = rdlane_f(fr.oz, 0);
-    const float ax = rdlane_f(fr.dx, 0), ay = rdlane_f(fr.dy, 0), az = rdlane_f(fr.dz, 0);
-    const float do2 = (fr.ox - ox) * (fr.ox - ox) + (fr.oy - oy) * (fr.oy - oy) + (fr.oz - oz) * (fr.oz - oz);
+    const bool cone = S.cull && wave_ok && exec_full() && !__any(valid && !fin) && tmin >= RV(0.0);
+    const float ox = rdlane_f(fr.ox, f), oy = rdlane_f(fr.oy, f), oz = rdlane_f(fr.oz, f);
+    const float ax = rdlane_f(fr.dx, f), ay = rdlane_f(fr.dy, f), az = rdlane_f(fr.dz, f);
+    const float do2 = valid ? (fr.ox - ox) * (fr.ox - ox) + (fr.oy - oy) * (fr.oy - oy) + (fr.oz - oz) * (fr.oz - oz)
+                            : 0.0f;
     // 1 - cos(angle to the axis), >= 0 up to rounding
-    const float dc = __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, ax, __builtin_fmaf(fr.dy, ay, fr.dz * az)));
+    const float dc = valid ? __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, ax, __builtin_fmaf(fr.dy, ay, fr.dz * az)))
+                           : 0.0f;
     const float rho = cone ? sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(do2)))) : 0.0f;
     const float dcm = cone ? __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f : 2.0f;   // rounding of unit dots
     const float cth = 1.0f - dcm;
@@ -1753,12 +1767,11 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     const float ftmin = (float)tmin;
     for (int base = 0; base < S.n_objs; base += 64) {
         const int j = base + lane;
-        bool pass = false;
-        if (j < S.n_objs) {
-            const float4 c0 = S.ctab[2 * j], c1 = S.ctab[2 * j + 1];
-            const int type = __float_as_int(c1.x);
-            pass = type != 0 && (type != 2 || wide || cone_touch(c0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
-        }
+        const int jr = j < S.n_objs ? j : S.n_objs - 1;   // (see scene_occluded_wave)
+        const float4 c0 = S.ctab[2 * jr], c1 = S.ctab[2 * jr + 1];
+        const int type = __float_as_int(c1.x);
+        const bool pass = (j < S.n_objs) & (type != 0) &
+                          ((type != 2) | wide | cone_touch(c0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
         const int nc = S.n_objs - base;
         uint64_t m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
@@ -1768,7 +1781,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 const int k = S.objs[o].kind;
                 if (k != rtamd::OBJ_GROUP && k != rtamd::OBJ_NEVER && !((m >> (o - base)) & 1)) ++skipped;
             }
-            cnt_add(cnt, RT_OPC_CULLED, skipped);
+            if (valid) cnt_add(cnt, RT_OPC_CULLED, skipped);
         }
         while (m) {
             const int o = base + __builtin_ctzll(m);
@@ -1783,7 +1796,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
 #ifdef RT_NO_LEAF_MASK
             const bool use_mask = false;
             if (!wide && ob.npb > 0 && exec_full() && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
-                cnt.inc(RT_OPC_CULLED);
+                if (valid) cnt.inc(RT_OPC_CULLED);
                 cnt.pe(PH_OBJ_PREF);
                 continue;
             }
@@ -1794,7 +1807,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
                 const bool in = lane < ob.npb;
                 if (!__any(in && cone_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
-                    cnt.inc(RT_OPC_CULLED);
+                    if (valid) cnt.inc(RT_OPC_CULLED);
                     cnt.pe(PH_OBJ_PREF);
                     continue;
                 }
@@ -1802,8 +1815,8 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 const uint64_t b = __ballot(in && line_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
                 lmask = full ? b : ~0ull;
             }
-            if (S.cull && ob.has_bound && !__any(ball_touch(ob.fb, fr, ftmin, (float)closest))) {
-                cnt.inc(RT_OPC_CULLED);
+            if (S.cull && ob.has_bound && !__any(valid && ball_touch(ob.fb, fr, ftmin, (float)closest))) {
+                if (valid) cnt.inc(RT_OPC_CULLED);
                 cnt.pe(PH_OBJ_PREF);
                 continue;
             }
@@ -1815,6 +1828,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             if (csg_obj) cnt.pb(PH_PRIMARY_CSG);
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_PR_HIT);
+            cnt.gate(valid);
             if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt, lmask, use_mask)) {
                 closest = t;
                 win = o;
@@ -1822,12 +1836,15 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 wts = ts;
                 wcode = code;
             }
+            cnt.gate(true);
             cnt.pe(PH_OBJ_HIT);
             if (csg_obj) cnt.pe(PH_PRIMARY_CSG);
         }
     }
     if (win < 0) return false;
+    cnt.gate(valid);
     resolve_hit<EAGER>(S, win, r, tmin, wp, wts, wcode, best, cnt);
+    cnt.gate(true);
     t_best = closest;
     return true;
 }
@@ -2057,9 +2074,133 @@ struct Frame {
     int want_refr;
 };
 
+// Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack,
+// wave-synchronous (WV kernels with reflection / refraction): every lane of
+// the wave runs every step until the whole wave is done, and a lane whose
+// path has finished rides along with valid = false.  The exec mask therefore
+// stays full at the closest-hit and shadow queries of every bounce, so their
+// wave-level culls apply to secondary rays too (a lane-divergent loop would
+// leave only the lanes still bouncing active and every query would fall back
+// to testing all objects).  Each lane's arithmetic is the one of trace()
+// below, step for step.
+template <bool EAGER, bool DEEP, bool DL, class CT>
+__device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+    Frame stk[kMaxDepth];
+    int sp = 0;
+    int depth = 0;
+    const int limit = S.rec_limit;
+    V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));
+    bool alive = true;
+    const bool wave_ok = __builtin_amdgcn_read_exec() == ~0ull;
+    while (__any(alive)) {
+        // ---- evaluate node (r, depth) on the lanes still tracing
+        const bool eval = alive && depth < limit;
+        if (alive && !eval) ret = v3(RV(0.0), RV(0.0), RV(0.0));
+        real ht = RV(0.0);
+        DHit h;
+        h.p = h.n = v3(RV(0.0), RV(0.0), RV(0.0));
+        h.mat = -1;
+        h.ff = 1;
+        if (eval) ++n_isect;
+        cnt.pb(PH_PRIMARY);
+        const bool hit = scene_intersect_wave<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
+        cnt.pe(PH_PRIMARY);
+        const bool sh = eval && hit;
+        if (eval && !hit) ret = v3(S.bg[0], S.bg[1], S.bg[2]);
+        V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
+        if (__any(sh)) direct = shade<EAGER, DEEP, DL, true>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, sh);
+        bool descend = false;
+        if (sh) {
+            if (h.mat < 0) {
+                ret = direct;
+            } else {
+                const MatT* mat = &S.mats[h.mat];
+                const bool can = depth < limit - 1;
+                const bool want_refl = mat->kr > RV(0.0) && can;
+                bool want_refr = false;
+                DRay refr;
+                if (mat->kt > RV(0.0) && can) {
+                    const real eta = h.ff ? (S.medium_index / mat->refractive_index)
+                                          : (mat->refractive_index / S.medium_index);
+                    const V3 inc = normalized(r.d);
+                    const real cos_i = -dot3(inc, h.n);   // tracer.cpp:100-104
+                    const real st2 = eta * eta * dmax(RV(0.0), RV(1.0) - cos_i * cos_i);
+                    if (!(st2 >= RV(1.0))) {
+                        want_refr = true;
+                        const real cos_t = sqrt_r(RV(1.0) - st2);   // tracer.cpp:87-98
+                        const real k = eta * cos_i - cos_t;
+                        const V3 rd = normalized(v3(inc.x * eta + h.n.x * k, inc.y * eta + h.n.y * k,
+                                                    inc.z * eta + h.n.z * k));
+                        const V3 ro = h.ff ? v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6))
+                                           : v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6));
+                        refr = make_ray(ro, rd);
+                    }
+                }
+                if (want_refl || want_refr) {
+                    Frame fr;
+                    fr.total = direct;
+                    fr.mat = h.mat;
+                    fr.want_refr = want_refr;
+                    fr.refr = refr;
+                    if (want_refl) {
+                        cnt.inc(RT_OPC_SECONDARY);
+                        const V3 inc = normalized(r.d);
+                        const real k = RV(2.0) * dot3(inc, h.n);   // reflect (tracer.cpp:76-78)
+                        const V3 rd = normalized(v3(inc.x - h.n.x * k, inc.y - h.n.y * k, inc.z - h.n.z * k));
+                        const V3 ro = h.ff ? v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6))
+                                           : v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6));
+                        fr.stage = 0;
+                        stk[sp++] = fr;
+                        r = make_ray(ro, rd);
+                    } else {
+                        cnt.inc(RT_OPC_SECONDARY);
+                        fr.stage = 1;
+                        stk[sp++] = fr;
+                        r = refr;
+                    }
+                    depth = sp;
+                    descend = true;
+                } else {
+                    ret = direct;
+                }
+            }
+        }
+        if (alive && !descend) {
+            // ---- unwind
+            bool resumed = false;
+            while (sp > 0) {
+                Frame& fr = stk[sp - 1];
+                const MatT* mat = &S.mats[fr.mat];
+                if (fr.stage == 0) {
+                    fr.total = combine(fr.total, v3(ret.x * mat->kr, ret.y * mat->kr, ret.z * mat->kr));
+                    if (fr.want_refr) {
+                        cnt.inc(RT_OPC_SECONDARY);
+                        fr.stage = 1;
+                        r = fr.refr;
+                        depth = sp;
+                        resumed = true;
+                        break;
+                    }
+                    ret = fr.total;
+                    --sp;
+                } else {
+                    fr.total = combine(fr.total, v3(ret.x * mat->kt, ret.y * mat->kt, ret.z * mat->kt));
+                    ret = fr.total;
+                    --sp;
+                }
+            }
+            if (!resumed) alive = false;
+        }
+    }
+    return ret;
+}
+
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
 template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, bool WV, class CT>
 __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+#ifndef RT_OLD_TRACE
+    if constexpr (SECONDARY && WV) return trace_wave<EAGER, DEEP, DL>(S, r, n_isect, n_occl, cnt);
+#endif
     if constexpr (!SECONDARY) {
         // No material reflects or refracts (or recursion <= 1): trace_recursive
         // reduces to one closest hit + local shading (tracer.cpp:22-37, 72).

@@ -156,6 +156,17 @@ __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_
     std_body<false, false, false, C, false, WV>(S, P);
 }
 
+// Reflection / refraction with wave-level culling (trace_wave): the wave
+// runs every bounce in lockstep.  Occupancy target RT_SEC_WAVES waves/SIMD.
+#ifndef RT_SEC_WAVES
+#define RT_SEC_WAVES 4
+#endif
+template <bool C>
+__global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_SEC_WAVES))) void k_std_secw(DevScene S,
+                                                                                                      StdParams P) {
+    std_body<false, false, true, C, false, true>(S, P);   // (no directional lights: those scenes take D)
+}
+
 template <bool E, bool D, bool C, bool DL = true, bool WV = false>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
@@ -363,8 +374,12 @@ void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneVie
         else launch_std_c<false, true, false>(c, grid, st, S, P);
     } else {
         if (sec) {
-            if (wv) launch_std_c<false, false, true, true>(c, grid, st, S, P);
-            else launch_std_c<false, false, true>(c, grid, st, S, P);
+            if (wv) {
+                if (c) hipLaunchKernelGGL((k_std_secw<true>), grid, dim3(kStdThreads), 0, st, S, P);
+                else hipLaunchKernelGGL((k_std_secw<false>), grid, dim3(kStdThreads), 0, st, S, P);
+            } else {
+                launch_std_c<false, false, true>(c, grid, st, S, P);
+            }
         } else if (wv) {
             if (c) hipLaunchKernelGGL((k_std_lean<true, true>), grid, dim3(kStdThreads), 0, st, S, P);
             else hipLaunchKernelGGL((k_std_lean<false, true>), grid, dim3(kStdThreads), 0, st, S, P);
@@ -404,7 +419,7 @@ const void* std_kernel(bool e, bool d, bool sec, bool wv) {
 #else
     if (e) return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
     if (d) return sec ? (const void*)k_std<false, true, true, false> : (const void*)k_std<false, true, false, false>;
-    if (sec) return wv ? (const void*)k_std<false, false, true, false, true> : (const void*)k_std<false, false, true, false>;
+    if (sec) return wv ? (const void*)k_std_secw<false> : (const void*)k_std<false, false, true, false>;
     return wv ? (const void*)k_std_lean<false, true> : (const void*)k_std_lean<false, false>;
 #endif
 }

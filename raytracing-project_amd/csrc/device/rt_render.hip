@@ -951,10 +951,11 @@ extern "C" int rt_test_kernel_name(const rt_scene* s, int mode, int flags, char*
                 name = std::string("k_paper_primary<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(cnt) + ">";
         } else if (!big && !eager && !deep && !secondary) {
             name = std::string("k_std_lean<") + tf(cnt) + ", " + tf(wv) + ">";
+        } else if (!big && !eager && !deep && wv) {   // (secondary here)
+            name = std::string("k_std_secw<") + tf(cnt) + ">";
         } else {
-            const bool w = !big && !eager && !deep && wv;   // the WV general variant exists for sec only
             name = std::string("k_std<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(secondary) + ", " +
-                   tf(cnt) + ", " + tf(w) + ">";
+                   tf(cnt) + ", false>";
         }
         std::snprintf(out, (size_t)cap, "%s::%s", ns, name.c_str());
         return RT_OK;

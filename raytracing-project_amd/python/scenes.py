@@ -121,6 +121,10 @@ CONFIGS = {
     3: ("pokeballs 1920x1080, 5 lights, rec 3 (config 3)", cfg3_scene, 0),
     4: ("snorlax 3840x2160, 5 lights, rec 4 (config 4)", cfg4_scene, 0),
     5: ("synthetic 7680x4320 64 spheres, 8 lights, rec 6, paper (config 5)", cfg5_scene, 1),
+    # not a BASELINE config: config 5's scene in STANDARD mode at 3840x2160, the
+    # reflection / refraction recursion (tracer.cpp:22-73) at scale
+    6: ("config-5 scene, standard mode 3840x2160, 8 lights, rec 6 (recursion row)",
+        lambda: with_dpi(cfg5_scene(), 960), 0),
 }
 
 

@@ -170,6 +170,29 @@ def test_counting_pass_with_cull_matches_plain(gpu, name, mode):
     assert s1.ops[gpu.OP_NAMES.index("light_eval")] > 0
 
 
+# Counters that do not depend on culling (shading calls, light evaluations,
+# lit lights, specular terms, reflection / refraction rays) must agree between
+# the culled counting kernel (for recursive scenes: trace_wave, where finished
+# lanes ride along with valid = false and must count nothing) and the unculled
+# one, whose counts equal the reference's (test_opcounts_match_reference_without_cull).
+CULL_FREE_OPS = ("shade_call", "light_eval", "shade_light", "shade_spec", "secondary")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg5", "reflect_refract", "snorlax", "cfg4"])
+def test_cull_independent_counts_match_unculled(gpu, name):
+    sc = gpu.load_scene_from_json_text(SMALL[name]())
+    W, H = sc.width, sc.height
+    s0, s1 = gpu.Stats(), gpu.Stats()
+    a = gpu.Tracer(sc, W, H, 0, flags=gpu.RT_FLAG_COUNT_OPS).render(s0)
+    b = gpu.Tracer(sc, W, H, 0, flags=gpu.RT_FLAG_COUNT_OPS | gpu.RT_FLAG_NO_CULL).render(s1)
+    assert np.array_equal(a, b)
+    for op in CULL_FREE_OPS:
+        k = gpu.OP_NAMES.index(op)
+        assert s0.ops[k] == s1.ops[k], (op, s0.ops[k], s1.ops[k])
+    assert (s0.rays_intersect, s0.rays_occluded) == (s1.rays_intersect, s1.rays_occluded)
+
+
 @pytest.mark.gpu
 def test_counting_pass_with_cull_matches_plain_midres(gpu):
     sc = gpu.load_scene_from_json_text(MID["cfg4_320"]())
