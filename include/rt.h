@@ -223,9 +223,11 @@ enum rt_flags {
     RT_FLAG_NONE = 0,
     RT_FLAG_COUNT_OPS = 1,      /* fill rt_stats.ops (slower, instrumented kernels) */
     RT_FLAG_NO_CULL = 2,        /* disable wave-uniform bounding-sphere culling    */
-    RT_FLAG_FP32 = 4            /* NON-PARITY fast path: trace in
+    RT_FLAG_FP32 = 4,           /* NON-PARITY fast path: trace in
                                    FP32 on float copies of the scene; framebuffer stays
                                    double.  Not within the 1e-5 parity tolerance.   */
+    RT_FLAG_NO_BVH = 8          /* scenes of more than 64 objects: wave-level culling
+                                   without the wave BVH (A/B; results are identical) */
 };
 
 /* Tracer::render: render the whole frame into a caller-owned host buffer of

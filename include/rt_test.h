@@ -33,6 +33,14 @@ int rt_test_jitter_device(int K_blocks, int64_t q0, int64_t q1, int64_t first, i
 struct rt_scene;
 int rt_test_compile_info(const struct rt_scene* s, int32_t* out);
 
+/* Host-only: the wave BVH of a scene (CompiledScene::wobjs ...).  counts[2] =
+ * {objects in the wave list, chunks} (both 0: no BVH); up to cap_objs
+ * entries of worig (each listed object's index in the compiled object table)
+ * and of wctab (8 floats per object: its cull record), up to cap_chunks
+ * chunk records (8 floats each). */
+int rt_test_wave_bvh(const struct rt_scene* s, int32_t* counts, int32_t* worig, float* wctab, int cap_objs,
+                     float* wchunk, int cap_chunks);
+
 /* Resources of the trace kernel rt_render would launch for this scene, mode
  * and flags (hipFuncGetAttributes + occupancy query): out[8] = {VGPRs per
  * lane, scratch bytes per lane, static LDS bytes per workgroup, resident

@@ -71,6 +71,13 @@ __device__ __forceinline__ real dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y 
 __device__ __forceinline__ real dmax(real a, real b) { return (a < b) ? b : a; }   // std::max
 __device__ __forceinline__ real dmin(real a, real b) { return (b < a) ? b : a; }   // std::min
 __device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+// The next representable value above x >= 0 (x itself for +inf).
+__device__ __forceinline__ double next_up(double x) {
+    return x < __builtin_inf() ? __longlong_as_double(__double_as_longlong(x) + 1) : x;
+}
+__device__ __forceinline__ float next_up(float x) {
+    return x < __builtin_inff() ? __int_as_float(__float_as_int(x) + 1) : x;
+}
 
 // (a0, a1, a2) / b: three IEEE divisions, bit-identical to the compiler's
 // own FP64 division (v_div_scale / v_rcp / two Newton steps / v_div_fmas /
@@ -288,6 +295,12 @@ struct DevScene {
     int rec_limit, cull;
     real eye[3], P[3], Lx, Ly;
     real bg[3], amb[3], medium_index;
+    // wave BVH kernels only (objs / ctab then hold CompiledScene::wobjs /
+    // wctab): each object's index in the reference's order, and the chunk
+    // records (2 x float4 per chunk of 64 objects)
+    const int32_t* worig;
+    const float4* wchunk;
+    int n_chunks;
 };
 
 __device__ __forceinline__ V3 ld3(const real* p) { return v3(p[0], p[1], p[2]); }
@@ -1543,7 +1556,13 @@ __device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, f
 // test's 1e-5 margins), and the exact FP64 ray (make_ray, one sqrt and three
 // divisions per lane) is formed only when some candidate object survives the
 // culls and is evaluated - most shadow queries of a wave end before that.
-template <bool EAGER, bool DEEP, bool UO, class CT>
+//
+// BV (wave BVH kernels): S.objs is the Morton-ordered list in chunks of 64
+// with a cull record per chunk (CompiledScene::wobjs / wchunk); one
+// transposed test per 64 chunks skips every chunk no querying segment can
+// reach, then each surviving chunk runs the object test below.  Occlusion is
+// an OR over objects, so the order is free.
+template <bool EAGER, bool DEEP, bool UO, bool BV = false, class CT>
 __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
 #if defined(RT_ABL) && RT_ABL == 1   // diagnostic ablation builds only (wrong images): no shadow queries
@@ -1583,7 +1602,20 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
     float lox = 0.0f, loy = 0.0f, loz = 0.0f, lax = 0.0f, lay = 0.0f, laz = 0.0f;
     float lrho = 0.0f, lcth = -1.0f, lsth = 1.0f, lmag = 0.0f;
     bool hit = false;
-    for (int base = 0; base < S.n_objs; base += 64) {
+    const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
+    uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 some querying segment can reach
+    for (int ch = 0; ch < nch; ++ch) {
+        if constexpr (BV) {
+            if ((ch & 63) == 0) {
+                const int c = ch + lane;
+                const int cr = c < nch ? c : nch - 1;
+                const float4 k0 = S.wchunk[2 * cr], k1 = S.wchunk[2 * cr + 1];
+                const bool pass = (c < nch) & record_touch(k0, k1, ax, ay, az, bx, by, bz, ux, uy, uz, uu, rho, mag);
+                cm = (cap && exec_full()) ? __ballot(pass) : ~0ull;
+            }
+            if (!((cm >> (ch & 63)) & 1ull)) continue;
+        }
+        const int base = ch << 6;
         const int nc = S.n_objs - base;
         const int j = base + lane;
         // the object's cull record (CompiledScene::ctab): one 32-byte load on
@@ -1730,7 +1762,16 @@ __device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, f
 // valid = false: a lane that only keeps the wave fully active (trace_wave's
 // finished paths); its ray is left out of the bundle and of every test, its
 // result is garbage and its ops are not counted.
-template <bool EAGER, bool DEEP, class CT>
+//
+// BV (wave BVH kernels): the chunk test of scene_occluded_wave with the
+// cone.  Objects then come in Morton order, not the reference's, so every
+// object is evaluated with the range up to and INCLUDING the closest hit so
+// far (each object's hit t does not depend on tmax, only its acceptance),
+// and a hit at exactly the closest t is resolved as the reference's in-order
+// loop would: of two objects hitting at the same t, the later (in the
+// reference's order) wins if it accepts t == tmax (spheres, half-spaces,
+// pokeballs: rtamd::accepts_tie), else the earlier one.
+template <bool EAGER, bool DEEP, bool BV = false, class CT>
 __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin, real tmax, real& t_best,
                                      DHit& best, bool wave_ok, CT& cnt, bool valid = true) {
     cnt.pb(PH_WAVE_SETUP);
@@ -1761,11 +1802,27 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     const int lane = __lane_id();
     real closest = tmax;
     int win = -1;
+    int win_orig = 0;       // (BV) the winner's index in the reference's order
+    bool win_tie = false;   // (BV) whether the winner accepts t == tmax
     V3 wp = v3(RV(0.0), RV(0.0), RV(0.0));
     real wts = RV(0.0);
     int wcode = 0;
     const float ftmin = (float)tmin;
-    for (int base = 0; base < S.n_objs; base += 64) {
+    const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
+    uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 the bundle can reach
+    for (int ch = 0; ch < nch; ++ch) {
+        if constexpr (BV) {
+            if ((ch & 63) == 0) {
+                const int c = ch + lane;
+                const int cr = c < nch ? c : nch - 1;
+                const float4 k0 = S.wchunk[2 * cr], k1 = S.wchunk[2 * cr + 1];
+                const int ktype = __float_as_int(k1.x);
+                const bool pass = (c < nch) & ((ktype != 2) | wide | cone_touch(k0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+                cm = (cone && exec_full()) ? __ballot(pass) : ~0ull;
+            }
+            if (!((cm >> (ch & 63)) & 1ull)) continue;
+        }
+        const int base = ch << 6;
         const int j = base + lane;
         const int jr = j < S.n_objs ? j : S.n_objs - 1;   // (see scene_occluded_wave)
         const float4 c0 = S.ctab[2 * jr], c1 = S.ctab[2 * jr + 1];
@@ -1829,7 +1886,23 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             cnt.pb(PH_OBJ_HIT);
             cnt.ev(EV_PR_HIT);
             cnt.gate(valid);
-            if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt, lmask, use_mask)) {
+            if constexpr (BV) {
+                const bool ok = object_hit<EAGER, DEEP>(S, ob, r, tmin, next_up(closest), t, p, ts, code, cnt, lmask,
+                                                        use_mask);
+                const int oo = S.worig[o];
+                const bool tie = rtamd::accepts_tie(ob);
+                const bool take = ok && ((t < closest) ||
+                                         (t == closest && (win < 0 ? tie : (oo > win_orig ? tie : !win_tie))));
+                if (take) {
+                    closest = t;
+                    win = o;
+                    win_orig = oo;
+                    win_tie = tie;
+                    wp = p;
+                    wts = ts;
+                    wcode = code;
+                }
+            } else if (object_hit<EAGER, DEEP>(S, ob, r, tmin, closest, t, p, ts, code, cnt, lmask, use_mask)) {
                 closest = t;
                 win = o;
                 wp = p;
@@ -1912,7 +1985,7 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 // never populates directional lights).
 // DL: the scene may have directional lights (the lean kernels, chosen only
 // for scenes without, do not carry their code or registers).
-template <bool EAGER, bool DEEP, bool DL, bool WV, bool UO = false, class CT>
+template <bool EAGER, bool DEEP, bool DL, int WV, bool UO = false, class CT>
 __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt,
                     bool valid = true) {
     // valid = false: a lane of the wave that has nothing to shade (a primary
@@ -1998,7 +2071,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             if constexpr (WV) {
                 cnt.pb(PH_SHADOW);
                 // (the direction's re-normalisation happens inside, when needed)
-                occ = scene_occluded_wave<EAGER, DEEP, UO>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
+                occ = scene_occluded_wave<EAGER, DEEP, UO, (WV == 2)>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
                 cnt.pe(PH_SHADOW);
             } else {
                 const DRay sr = make_ray(so, wi);
@@ -2083,7 +2156,7 @@ struct Frame {
 // leave only the lanes still bouncing active and every query would fall back
 // to testing all objects).  Each lane's arithmetic is the one of trace()
 // below, step for step.
-template <bool EAGER, bool DEEP, bool DL, class CT>
+template <bool EAGER, bool DEEP, bool DL, int WV, class CT>
 __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     Frame stk[kMaxDepth];
     int sp = 0;
@@ -2103,12 +2176,12 @@ __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t&
         h.ff = 1;
         if (eval) ++n_isect;
         cnt.pb(PH_PRIMARY);
-        const bool hit = scene_intersect_wave<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
+        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2)>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
         cnt.pe(PH_PRIMARY);
         const bool sh = eval && hit;
         if (eval && !hit) ret = v3(S.bg[0], S.bg[1], S.bg[2]);
         V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
-        if (__any(sh)) direct = shade<EAGER, DEEP, DL, true>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, sh);
+        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, sh);
         bool descend = false;
         if (sh) {
             if (h.mat < 0) {
@@ -2196,10 +2269,10 @@ __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t&
 }
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
-template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, bool WV, class CT>
+template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, int WV, class CT>
 __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
 #ifndef RT_OLD_TRACE
-    if constexpr (SECONDARY && WV) return trace_wave<EAGER, DEEP, DL>(S, r, n_isect, n_occl, cnt);
+    if constexpr (SECONDARY && WV) return trace_wave<EAGER, DEEP, DL, WV>(S, r, n_isect, n_occl, cnt);
 #endif
     if constexpr (!SECONDARY) {
         // No material reflects or refracts (or recursion <= 1): trace_recursive
@@ -2213,7 +2286,7 @@ __device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_oc
             // miss lanes stay in shade() (valid = false) so that the wave
             // stays fully active for the wave-level shadow queries
             cnt.pb(PH_PRIMARY);
-            const bool hit = scene_intersect_wave<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h,
+            const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2)>(S, r, RV(1e-4), RT_INF, ht, h,
                                                                __builtin_amdgcn_read_exec() == ~0ull, cnt);
             cnt.pe(PH_PRIMARY);
             if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);

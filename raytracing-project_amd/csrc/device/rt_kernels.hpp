@@ -95,7 +95,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #define RT_LEAN_WAVES 4
 #endif
 
-template <bool E, bool D, bool SEC, bool C, bool DL = true, bool WV = false>
+template <bool E, bool D, bool SEC, bool C, bool DL = true, int WV = 0>
 __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -150,7 +150,9 @@ __global__ __launch_bounds__(kStdThreads) void k_std(DevScene S, StdParams P) {
     std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
-template <bool C, bool WV>
+// WV: 0 = per-lane culls, 1 = wave-level culls, 2 = wave-level culls over the
+// wave BVH (CompiledScene::wobjs / wchunk)
+template <bool C, int WV>
 __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
                                                                                                        StdParams P) {
     std_body<false, false, false, C, false, WV>(S, P);
@@ -161,13 +163,13 @@ __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_
 #ifndef RT_SEC_WAVES
 #define RT_SEC_WAVES 4
 #endif
-template <bool C>
+template <bool C, int WV = 1>
 __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_SEC_WAVES))) void k_std_secw(DevScene S,
                                                                                                       StdParams P) {
-    std_body<false, false, true, C, false, true>(S, P);   // (no directional lights: those scenes take D)
+    std_body<false, false, true, C, false, WV>(S, P);   // (no directional lights: those scenes take D)
 }
 
-template <bool E, bool D, bool C, bool DL = true, bool WV = false>
+template <bool E, bool D, bool C, bool DL = true, int WV = 0>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
@@ -193,7 +195,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         r = gen_ray(S, x, y);
         ++ni;
         if constexpr (WV)
-            hits = scene_intersect_wave<E, D>(S, r, RV(1e-4), RT_INF, ht, h, __builtin_amdgcn_read_exec() == ~0ull,
+            hits = scene_intersect_wave<E, D, (WV == 2)>(S, r, RV(1e-4), RT_INF, ht, h, __builtin_amdgcn_read_exec() == ~0ull,
                                               cnt);
         else
             hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
     paper_primary_body<E, D, C>(S, P);
 }
 
-template <bool C, bool WV>
+template <bool C, int WV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
     paper_primary_body<false, false, C, false, WV>(S, P);
@@ -309,21 +311,25 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     dst[2] = o.z;
 }
 
-DevScene make_scene(const SceneView& V) {
+// bv: the wave BVH kernels, whose object list is the Morton-ordered one
+DevScene make_scene(const SceneView& V, bool bv = false) {
     DevScene S;
     S.nodes = static_cast<const NodeT*>(V.nodes);
     S.mats = static_cast<const MatT*>(V.mats);
     S.lights = static_cast<const LightT*>(V.lights);
     S.dlights = static_cast<const DLightT*>(V.dlights);
-    S.objs = V.objs;
+    S.objs = bv ? V.wobjs : V.objs;
     S.ops = V.ops;
     S.gb = V.gb;
-    S.ctab = reinterpret_cast<const float4*>(V.ctab);
+    S.ctab = reinterpret_cast<const float4*>(bv ? V.wctab : V.ctab);
     S.fold = static_cast<const FoldT*>(V.fold);
+    S.worig = bv ? V.worig : nullptr;
+    S.wchunk = reinterpret_cast<const float4*>(bv ? V.wchunk : nullptr);
+    S.n_chunks = bv ? V.n_chunks : 0;
     S.n_lights = V.n_lights;
     S.n_dlights = V.n_dlights;
     S.n_bounded = V.n_bounded;
-    S.n_objs = V.n_objs;
+    S.n_objs = bv ? V.n_wobjs : V.n_objs;
     S.cam_nx = V.cam_nx;
     S.cam_ny = V.cam_ny;
     S.rec_limit = V.rec_limit;
@@ -356,7 +362,8 @@ void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const 
 
 // Eager scenes always use D.  Each variant gets its own register allocation.
 void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneView& V, const StdParams& P) {
-    const DevScene S = make_scene(V);
+    const bool bv = !e && !d && V.cull && V.n_bounded >= 4 && V.n_chunks > 0;
+    const DevScene S = make_scene(V, bv);
     const dim3 grid((P.W + kStdBlockX - 1) / kStdBlockX, (P.n_rows + kStdBlockY - 1) / kStdBlockY);
 #ifdef RT_GENERAL_ONLY
     // big-stack build: only the general variants (every feature, scratch stacks)
@@ -374,25 +381,32 @@ void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneVie
         else launch_std_c<false, true, false>(c, grid, st, S, P);
     } else {
         if (sec) {
-            if (wv) {
+            if (bv) {
+                if (c) hipLaunchKernelGGL((k_std_secw<true, 2>), grid, dim3(kStdThreads), 0, st, S, P);
+                else hipLaunchKernelGGL((k_std_secw<false, 2>), grid, dim3(kStdThreads), 0, st, S, P);
+            } else if (wv) {
                 if (c) hipLaunchKernelGGL((k_std_secw<true>), grid, dim3(kStdThreads), 0, st, S, P);
                 else hipLaunchKernelGGL((k_std_secw<false>), grid, dim3(kStdThreads), 0, st, S, P);
             } else {
                 launch_std_c<false, false, true>(c, grid, st, S, P);
             }
+        } else if (bv) {
+            if (c) hipLaunchKernelGGL((k_std_lean<true, 2>), grid, dim3(kStdThreads), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, 2>), grid, dim3(kStdThreads), 0, st, S, P);
         } else if (wv) {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, true>), grid, dim3(kStdThreads), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, true>), grid, dim3(kStdThreads), 0, st, S, P);
+            if (c) hipLaunchKernelGGL((k_std_lean<true, 1>), grid, dim3(kStdThreads), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, 1>), grid, dim3(kStdThreads), 0, st, S, P);
         } else {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, false>), grid, dim3(kStdThreads), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, false>), grid, dim3(kStdThreads), 0, st, S, P);
+            if (c) hipLaunchKernelGGL((k_std_lean<true, 0>), grid, dim3(kStdThreads), 0, st, S, P);
+            else hipLaunchKernelGGL((k_std_lean<false, 0>), grid, dim3(kStdThreads), 0, st, S, P);
         }
     }
 #endif
 }
 
 void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const SceneView& V, const PaperParams& P) {
-    const DevScene S = make_scene(V);
+    const bool bv = !e && !d && V.cull && V.n_bounded >= 4 && V.n_chunks > 0;
+    const DevScene S = make_scene(V, bv);
 #ifdef RT_GENERAL_ONLY
     (void)e;
     (void)d;
@@ -401,37 +415,40 @@ void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const Scene
     const bool wv = V.cull && V.n_bounded >= 4;
     if (e) launch_paper_c<true, true>(c, grid, st, S, P);
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
-    else if (wv) {
-        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary_lean<false, true>), grid, dim3(256), 0, st, S, P);
+    else if (bv) {
+        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 2>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, 2>), grid, dim3(256), 0, st, S, P);
+    } else if (wv) {
+        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 1>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, 1>), grid, dim3(256), 0, st, S, P);
     } else {
-        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, false>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary_lean<false, false>), grid, dim3(256), 0, st, S, P);
+        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 0>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, 0>), grid, dim3(256), 0, st, S, P);
     }
 #endif
 }
 
 // The kernel launch_std / launch_paper pick for a variant (resource queries).
-const void* std_kernel(bool e, bool d, bool sec, bool wv) {
+const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv) {
 #ifdef RT_GENERAL_ONLY
-    (void)e, (void)d, (void)wv;
+    (void)e, (void)d, (void)wv, (void)bv;
     return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
 #else
     if (e) return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
     if (d) return sec ? (const void*)k_std<false, true, true, false> : (const void*)k_std<false, true, false, false>;
-    if (sec) return wv ? (const void*)k_std_secw<false> : (const void*)k_std<false, false, true, false>;
-    return wv ? (const void*)k_std_lean<false, true> : (const void*)k_std_lean<false, false>;
+    if (sec) return bv ? (const void*)k_std_secw<false, 2> : wv ? (const void*)k_std_secw<false> : (const void*)k_std<false, false, true, false>;
+    return bv ? (const void*)k_std_lean<false, 2> : wv ? (const void*)k_std_lean<false, 1> : (const void*)k_std_lean<false, 0>;
 #endif
 }
 
-const void* paper_kernel(bool e, bool d, bool wv) {
+const void* paper_kernel(bool e, bool d, bool wv, bool bv) {
 #ifdef RT_GENERAL_ONLY
-    (void)e, (void)d, (void)wv;
+    (void)e, (void)d, (void)wv, (void)bv;
     return (const void*)k_paper_primary<true, true, false>;
 #else
     if (e) return (const void*)k_paper_primary<true, true, false>;
     if (d) return (const void*)k_paper_primary<false, true, false>;
-    return wv ? (const void*)k_paper_primary_lean<false, true> : (const void*)k_paper_primary_lean<false, false>;
+    return bv ? (const void*)k_paper_primary_lean<false, 2> : wv ? (const void*)k_paper_primary_lean<false, 1> : (const void*)k_paper_primary_lean<false, 0>;
 #endif
 }
 

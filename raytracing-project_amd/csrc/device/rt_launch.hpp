@@ -71,6 +71,12 @@ struct SceneView {
     const float* gb;
     const float* ctab;   // CompiledScene::ctab
     const void* fold;   // FoldLeafR of the launching precision
+    // wave BVH (CompiledScene::wobjs, wctab, worig, wchunk); n_chunks = 0: none
+    const DevObj* wobjs;
+    const float* wctab;
+    const int32_t* worig;
+    const float* wchunk;
+    int n_wobjs, n_chunks;
     int n_lights, n_dlights, n_objs;
     int n_bounded;
     int cam_nx, cam_ny;
@@ -136,8 +142,8 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
     void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,               \
                       const rtamd::PaperParams& P);                                                               \
     void launch_paper_finish(dim3 grid, hipStream_t st, const rtamd::PaperParams& P);                             \
-    const void* std_kernel(bool e, bool d, bool sec, bool wv);                                                    \
-    const void* paper_kernel(bool e, bool d, bool wv);                                                            \
+    const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv);                                           \
+    const void* paper_kernel(bool e, bool d, bool wv, bool bv);                                                   \
     }
 RT_DECLARE_LAUNCHERS(rtd)
 RT_DECLARE_LAUNCHERS(rtf)

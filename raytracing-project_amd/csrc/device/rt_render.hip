@@ -119,6 +119,7 @@ struct SceneCache {
 struct Workspace {
     std::mutex mu;
     DBuf nodes, mats, lights, dlights, objs, ops, gb, ctab;
+    DBuf wobjs, wctab, worig, wchunk;   // wave BVH (CompiledScene::wobjs ...)
     DBuf fold;
     DBuf nodes_f, mats_f, lights_f, dlights_f, fold_f;   // float copies (RT_FLAG_FP32)
     DBuf rows, jit, ckpt, jscratch, counters;
@@ -319,6 +320,10 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(upload(ws.ops, sc.cs.ops, st));
         HIP_TRY(upload(ws.gb, sc.cs.gbounds, st));
         HIP_TRY(upload(ws.ctab, sc.cs.ctab, st));
+        HIP_TRY(upload(ws.wobjs, sc.cs.wobjs, st));
+        HIP_TRY(upload(ws.wctab, sc.cs.wctab, st));
+        HIP_TRY(upload(ws.worig, sc.cs.worig, st));
+        HIP_TRY(upload(ws.wchunk, sc.cs.wchunk, st));
         sc.uid = rtamd::scene_uid(s);
         sc.fp32 = fp32;
         sc.valid = true;
@@ -380,6 +385,12 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.ops = ws.ops.as<rtamd::DevOp>();
     S.gb = ws.gb.as<float>();
     S.ctab = ws.ctab.as<float>();
+    S.wobjs = ws.wobjs.as<rtamd::DevObj>();
+    S.wctab = ws.wctab.as<float>();
+    S.worig = ws.worig.as<int32_t>();
+    S.wchunk = ws.wchunk.as<float>();
+    S.n_wobjs = (int)cs.wobjs.size();
+    S.n_chunks = (flags & RT_FLAG_NO_BVH) ? 0 : (int)(cs.wchunk.size() / 8);
     S.n_lights = d.n_lights;
     S.n_objs = (int)cs.objs.size();
     S.n_bounded = 0;
@@ -677,6 +688,7 @@ int rtamd::release_device_workspaces() {
         (void)hipSetDevice((int)dev);
         (void)hipDeviceSynchronize();
         for (DBuf* b : {&w->nodes, &w->mats, &w->lights, &w->dlights, &w->objs, &w->ops, &w->gb, &w->ctab, &w->fold,
+                        &w->wobjs, &w->wctab, &w->worig, &w->wchunk,
                         &w->nodes_f, &w->mats_f, &w->lights_f, &w->dlights_f, &w->fold_f, &w->rows, &w->jit, &w->ckpt,
                         &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb})
             b->release();
@@ -937,6 +949,7 @@ extern "C" int rt_test_kernel_name(const rt_scene* s, int mode, int flags, char*
             if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
         const bool f32 = (flags & RT_FLAG_FP32) != 0;
         const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
+        const bool bv = wv && !cs.wchunk.empty() && !(flags & RT_FLAG_NO_BVH);
         const bool cnt = (flags & RT_FLAG_COUNT_OPS) != 0;
         const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
         const bool big = !f32 && (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2 ||
@@ -946,13 +959,13 @@ extern "C" int rt_test_kernel_name(const rt_scene* s, int mode, int flags, char*
         std::string name;
         if (mode == RT_MODE_PAPER) {
             if (!big && !eager && !deep)
-                name = std::string("k_paper_primary_lean<") + tf(cnt) + ", " + tf(wv) + ">";
+                name = std::string("k_paper_primary_lean<") + tf(cnt) + ", " + (bv ? "2" : wv ? "1" : "0") + ">";
             else
                 name = std::string("k_paper_primary<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(cnt) + ">";
         } else if (!big && !eager && !deep && !secondary) {
-            name = std::string("k_std_lean<") + tf(cnt) + ", " + tf(wv) + ">";
+            name = std::string("k_std_lean<") + tf(cnt) + ", " + (bv ? "2" : wv ? "1" : "0") + ">";
         } else if (!big && !eager && !deep && wv) {   // (secondary here)
-            name = std::string("k_std_secw<") + tf(cnt) + ">";
+            name = std::string("k_std_secw<") + tf(cnt) + ", " + (bv ? "2" : "1") + ">";
         } else {
             name = std::string("k_std<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(secondary) + ", " +
                    tf(cnt) + ", false>";
@@ -981,16 +994,18 @@ extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32
         for (const auto& o : cs.objs)
             if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
         const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
+        const bool bv = wv && !cs.has_eager && !deep && !cs.wchunk.empty() && !(flags & RT_FLAG_NO_BVH);
         const bool f32 = (flags & RT_FLAG_FP32) != 0;
         const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
         const bool big = !f32 && (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2 ||
                                   frames > kMaxDepth);
-        const void* fn = big ? (mode == RT_MODE_PAPER ? rtdb::paper_kernel(true, true, false)
-                                                      : rtdb::std_kernel(true, true, secondary, false))
+        const void* fn = big ? (mode == RT_MODE_PAPER ? rtdb::paper_kernel(true, true, false, false)
+                                                      : rtdb::std_kernel(true, true, secondary, false, false))
                        : mode == RT_MODE_PAPER
-                             ? (f32 ? rtf::paper_kernel(cs.has_eager, deep, wv) : rtd::paper_kernel(cs.has_eager, deep, wv))
-                             : (f32 ? rtf::std_kernel(cs.has_eager, deep, secondary, wv)
-                                    : rtd::std_kernel(cs.has_eager, deep, secondary, wv));
+                             ? (f32 ? rtf::paper_kernel(cs.has_eager, deep, wv, bv)
+                                    : rtd::paper_kernel(cs.has_eager, deep, wv, bv))
+                             : (f32 ? rtf::std_kernel(cs.has_eager, deep, secondary, wv, bv)
+                                    : rtd::std_kernel(cs.has_eager, deep, secondary, wv, bv));
         hipFuncAttributes a{};
         HIP_TRY(hipFuncGetAttributes(&a, fn));
         int blocks = 0;
@@ -1003,6 +1018,26 @@ extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32
         out[5] = a.maxThreadsPerBlock;
         out[6] = wv ? 1 : 0;
         out[7] = secondary ? 1 : 0;
+        return RT_OK;
+    } catch (const std::exception& e) {
+        rtamd::set_last_error(std::string("scene compile: ") + e.what());
+        return RT_ERR_INVALID_ARG;
+    }
+}
+
+extern "C" int rt_test_wave_bvh(const rt_scene* s, int32_t* counts, int32_t* worig, float* wctab, int cap_objs,
+                                float* wchunk, int cap_chunks) {
+    if (!s || !counts || cap_objs < 0 || cap_chunks < 0) return RT_ERR_INVALID_ARG;
+    try {
+        const rtamd::CompiledScene cs = rtamd::compile_scene(*rt_scene_get_desc(s));
+        const int n = (int)cs.wobjs.size(), nch = (int)(cs.wchunk.size() / 8);
+        counts[0] = n;
+        counts[1] = nch;
+        for (int i = 0; i < std::min(n, cap_objs); ++i) {
+            if (worig) worig[i] = cs.worig[i];
+            if (wctab) std::memcpy(wctab + 8 * (size_t)i, &cs.wctab[8 * (size_t)i], 8 * sizeof(float));
+        }
+        if (wchunk) std::memcpy(wchunk, cs.wchunk.data(), (size_t)std::min(nch, cap_chunks) * 8 * sizeof(float));
         return RT_OK;
     } catch (const std::exception& e) {
         rtamd::set_last_error(std::string("scene compile: ") + e.what());

@@ -459,7 +459,99 @@ public:
             }
             std::memcpy(&c[4], &type, sizeof(int));
         }
+        build_wave_bvh(cs);
         return cs;
+    }
+
+    // The wave BVH (CompiledScene::wobjs ...).  Morton order of the f32 bound
+    // centres over their bounding box (10 bits per axis) puts nearby objects
+    // in the same chunk, so a chunk's enclosing ball is tight and one
+    // transposed test over the chunk records skips whole chunks of objects.
+    static void build_wave_bvh(CompiledScene& cs) {
+        std::vector<int> ids;
+        for (size_t j = 0; j < cs.objs.size(); ++j)
+            if (cs.objs[j].kind != OBJ_GROUP && cs.objs[j].kind != OBJ_NEVER) ids.push_back((int)j);
+        // (up to four chunks the transposed object test alone is as cheap:
+        // 145 objects ran 8 % slower with the BVH, profiles/r03g_bvh_perf.txt)
+        if (cs.has_eager || (int)ids.size() <= kWaveBvhMin) return;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int j : ids)
+            if (cs.objs[j].has_bound)
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::min(lo[k], cs.objs[j].bc[k]);
+                    hi[k] = std::max(hi[k], cs.objs[j].bc[k]);
+                }
+        auto spread = [](uint32_t v) {   // 10 bits -> every third bit
+            v &= 0x3ffu;
+            v = (v | (v << 16)) & 0x030000ffu;
+            v = (v | (v << 8)) & 0x0300f00fu;
+            v = (v | (v << 4)) & 0x030c30c3u;
+            v = (v | (v << 2)) & 0x09249249u;
+            return v;
+        };
+        auto morton = [&](const DevObj& o) -> uint64_t {
+            if (!o.has_bound) return 0;   // unbounded objects first (their chunks are never skipped)
+            uint32_t code = 0;
+            for (int k = 0; k < 3; ++k) {
+                const double ext = hi[k] - lo[k];
+                const double u = ext > 0 ? (o.bc[k] - lo[k]) / ext : 0.0;
+                const uint32_t q = (uint32_t)std::min(1023.0, std::max(0.0, std::floor(u * 1024.0)));
+                code |= spread(q) << k;
+            }
+            return 1 + (uint64_t)code;
+        };
+        std::vector<std::pair<uint64_t, int>> keyed;
+        for (int j : ids) keyed.emplace_back(morton(cs.objs[j]), j);
+        std::stable_sort(keyed.begin(), keyed.end(),
+                         [](const std::pair<uint64_t, int>& a, const std::pair<uint64_t, int>& b) { return a.first < b.first; });
+        // the unbounded objects fill the first chunk(s), padded with
+        // never-hit entries so that every later chunk is all balls
+        size_t n_unb = 0;
+        while (n_unb < keyed.size() && keyed[n_unb].first == 0) ++n_unb;
+        const size_t pad = n_unb % kWaveChunk ? kWaveChunk - n_unb % kWaveChunk : 0;
+        const size_t n = keyed.size() + pad;
+        cs.wobjs.assign(n, DevObj{});
+        cs.worig.assign(n, -1);
+        cs.wctab.assign(n * 8, 0.0f);   // (type 0: never a candidate)
+        for (size_t i = n_unb; i < n_unb + pad; ++i) cs.wobjs[i].kind = OBJ_NEVER;
+        for (size_t k = 0; k < keyed.size(); ++k) {
+            const size_t i = k < n_unb ? k : k + pad;
+            const int j = keyed[k].second;
+            cs.wobjs[i] = cs.objs[j];
+            cs.worig[i] = j;
+            std::memcpy(&cs.wctab[8 * i], &cs.ctab[8 * (size_t)j], 8 * sizeof(float));
+        }
+        const size_t nch = (n + kWaveChunk - 1) / kWaveChunk;
+        cs.wchunk.assign(nch * 8, 0.0f);
+        for (size_t c = 0; c < nch; ++c) {
+            const size_t a = c * kWaveChunk, b = std::min(n, a + kWaveChunk);
+            bool all_bounded = true;
+            double C[3] = {0.0, 0.0, 0.0};
+            size_t cnt = 0;
+            for (size_t i = a; i < b; ++i) {
+                if (cs.wobjs[i].kind == OBJ_NEVER) continue;   // (padding)
+                all_bounded = all_bounded && cs.wobjs[i].has_bound;
+                for (int k = 0; k < 3; ++k) C[k] += cs.wobjs[i].bc[k];
+                ++cnt;
+            }
+            float* rec = &cs.wchunk[8 * c];
+            int type = 1;
+            if (all_bounded && cnt > 0) {
+                for (int k = 0; k < 3; ++k) C[k] /= (double)cnt;
+                double R = 0.0;
+                for (size_t i = a; i < b; ++i) {
+                    const DevObj& o = cs.wobjs[i];
+                    if (o.kind == OBJ_NEVER) continue;
+                    const double dx = o.bc[0] - C[0], dy = o.bc[1] - C[1], dz = o.bc[2] - C[2];
+                    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + o.br);
+                }
+                const double mag = std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + R;
+                R = R * (1.0 + 1e-7) + 1e-7 * (1.0 + mag);
+                float_ball(C, R, rec);
+                type = 2;
+            }
+            std::memcpy(&rec[4], &type, sizeof(int));
+        }
     }
 
     // Wave-uniform cull groups over runs of consecutive bounded objects.  A run

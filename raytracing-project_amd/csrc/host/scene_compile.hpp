@@ -95,11 +95,38 @@ struct CompiledScene {
     std::vector<float> ctab;
     std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated;
                                    // then the leaf prefilter balls of CHAIN objects (world frame, see DevObj::pb0)
+    // Wave BVH (scenes with more than kWaveChunk objects and no eager
+    // programs; DESIGN.md §Wave BVH): the wave kernels' object list - every
+    // object except group headers and never-hit objects, unbounded ones
+    // first, the rest in Morton order of their bound centres - with its cull
+    // records, each object's index in objs (the reference's order, which
+    // decides closest-hit ties) and one cull record per chunk of kWaveChunk
+    // consecutive objects (the enclosing ball; type 1 = always a candidate
+    // for a chunk with an unbounded member).  Empty: no BVH.
+    std::vector<DevObj> wobjs;
+    std::vector<float> wctab;
+    std::vector<int32_t> worig;
+    std::vector<float> wchunk;
     int max_ray_depth = 0;   // transform nesting on any path of an eager program (chains need no stack)
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter
     bool has_pokeball = false;
 };
+
+constexpr int kWaveChunk = 64;   // objects per transposed test (one wave)
+constexpr int kWaveBvhMin = 4 * kWaveChunk;   // the wave BVH is built for scenes of more objects
+
+// Closest-hit tie rule of Scene::intersect (scene.cpp:10-24) for an object:
+// does it accept a hit at t == tmax (a later such object replaces an earlier
+// one at the same t)?  Spheres, half-spaces and pokeballs do (geometry.cpp
+// range tests), a CSG or a transform does not (strict t < tmax).
+#ifdef __HIP__
+__host__ __device__
+#endif
+inline bool accepts_tie(const DevObj& o) {
+    return o.kind == OBJ_SPHERE || o.kind == OBJ_HALF || o.kind == OBJ_POKE ||
+           (o.kind == OBJ_CHAIN && o.m == 0 && o.core == 0);
+}
 
 // Throws std::runtime_error on malformed IR.
 CompiledScene compile_scene(const rt_scene_desc& d);

@@ -115,6 +115,74 @@ def cfg5_scene() -> dict:
     }
 
 
+def bvh_scenes(dpi: int = 16) -> dict[str, dict]:
+    """Scenes of more than one wave's 64 objects, for the wave BVH
+    (CompiledScene::wobjs; tests/test_gpu_bvh.py):
+      grid  576 spheres on a 24 x 24 lattice over a floor (every 5th
+            reflective, every 7th refractive), 4 lights;
+      ties  exact closest-hit ties between objects of both acceptance rules:
+            pairs of coincident spheres, some wrapped in a CSG union with a
+            tiny far sphere (its first hit t is the same double as the bare
+            sphere's, its bound centre lies far away, so Morton order and the
+            reference's order disagree about which of a pair comes first):
+            sphere vs union (the sphere wins), union vs union (the earlier
+            wins), sphere vs sphere (the later wins), in both orders and
+            different colours."""
+    def mat(k):
+        m = _mat([(k % 7) / 7.0, (k % 5) / 5.0, (k % 3) / 3.0], shininess=8 + 4 * (k % 5))
+        if k % 5 == 0:
+            m["reflected"] = [0.4, 0.4, 0.4]
+        elif k % 7 == 0:
+            m["refracted"] = [0.5, 0.5, 0.5]
+        return m
+
+    lights = [{"position": [4, 6, 3], "intensity": [30, 30, 30]}, {"position": [-5, 5, 2], "intensity": [20, 20, 20]},
+              {"position": [0, 8, -4], "intensity": [15, 15, 15]}, {"position": [2, 1, 4], "intensity": [10, 10, 10]}]
+    grid = [{"halfSpace": {"position": [0, -1.4, 0], "normal": [0, 1, 0], "color": _mat([0.6, 0.6, 0.6])}}]
+    for k in range(576):
+        i, j = k % 24, k // 24
+        grid.append({"sphere": {"position": [-3.45 + 0.3 * i, -1.2 + 0.05 * (i % 3), -1.5 - 0.3 * j],
+                                "radius": 0.1 + 0.03 * ((i + j) % 3), "color": mat(k), "index": 1.5}})
+    ties = [{"halfSpace": {"position": [0, -1.4, 0], "normal": [0, 1, 0], "color": _mat([0.5, 0.5, 0.5])}}]
+    for k in range(150):
+        i, j = k % 15, k // 15
+        c = [-3.5 + 0.5 * i, -1.0 + 0.3 * j, -2.5 - 0.5 * j]
+        r = 0.18 + 0.04 * (k % 3)
+
+        def bare(col):
+            return {"sphere": {"position": list(c), "radius": r, "color": _mat(col)}}
+
+        def wrapped(col, side):
+            far = {"sphere": {"position": [c[0] + 40.0 * side, c[1] + 30.0, c[2] - 60.0], "radius": 0.01,
+                              "color": _mat([0.5, 0.5, 0.5])}}
+            return {"union": [{"sphere": {"position": list(c), "radius": r, "color": _mat(col)}}, far]}
+
+        if k % 3 == 0:     # sphere vs union: the sphere wins either way
+            pair = [bare([1.0, 0.1, 0.1]), wrapped([0.1, 1.0, 0.1], 1)]
+        elif k % 3 == 1:   # union vs union: the earlier one wins
+            pair = [wrapped([0.1, 1.0, 0.1], 1), wrapped([0.1, 0.1, 1.0], -1)]
+        else:              # sphere vs sphere: the later one wins
+            pair = [bare([1.0, 0.1, 0.1]), bare([1.0, 1.0, 0.1])]
+        ties += pair if (k // 3) % 2 == 0 else pair[::-1]
+    return {"grid": _base(grid, recursion=3, dpi=dpi, lights=lights),
+            "ties": _base(ties, recursion=2, dpi=dpi, lights=lights[:2])}
+
+
+def bvh_perf_scene(n: int = 4096, seed: int = 7, dpi: int = 480) -> dict:
+    """n random spheres (seeded) over a floor, 4 lights, recursion 1, at
+    dpi 480 (1920x1080): the wave BVH's perf case (tools/bvh_perf.py)."""
+    import random
+    rnd = random.Random(seed)
+    objs = [{"halfSpace": {"position": [0, -1.4, 0], "normal": [0, 1, 0], "color": _mat([0.6, 0.6, 0.6])}}]
+    for _ in range(n):
+        objs.append({"sphere": {"position": [rnd.uniform(-6, 6), rnd.uniform(-1.3, 2.5), rnd.uniform(-14, -1.5)],
+                                "radius": rnd.uniform(0.03, 0.12),
+                                "color": _mat([rnd.random(), rnd.random(), rnd.random()], shininess=rnd.choice([8, 16, 32]))}})
+    lights = [{"position": [4, 6, 3], "intensity": [30, 30, 30]}, {"position": [-5, 5, 2], "intensity": [20, 20, 20]},
+              {"position": [0, 8, -4], "intensity": [15, 15, 15]}, {"position": [2, 1, 4], "intensity": [10, 10, 10]}]
+    return _base(objs, recursion=1, dpi=dpi, lights=lights)
+
+
 CONFIGS = {
     1: ("penguin 1200x900 (config 1)", lambda: load_example("penguin"), 0),
     2: ("synthetic 640x480 3 spheres + halfSpace, 3 lights, rec 1 (config 2)", cfg2_scene, 0),

@@ -20,8 +20,10 @@ turned into IR by our loader (librt_host.so).  Outputs are data only:
                transforms, a 12-leaf right-nested csg), both modes
   crowd.npz    frames + counts of the seeded 150-object random scenes
                (scenes.crowd_scene, seeds 1-3), both modes
+  bvh.npz      frames + counts of the wave-BVH scenes (scenes.bvh_scenes:
+               a 576-sphere lattice, exact closest-hit ties), both modes
 
-Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights deep crowd]
+Usage: python tests/golden/make_golden.py [frames kats jitter cameras dirlights deep crowd bvh]
 """
 from __future__ import annotations
 
@@ -221,6 +223,20 @@ def make_crowd():
     print("crowd:", len(data))
 
 
+def make_bvh():
+    """Scenes of more than 64 objects for the wave BVH (scenes.bvh_scenes), both modes."""
+    data = {}
+    for name, scene in scenes.bvh_scenes(dpi=16).items():
+        sc = rtamd.load_scene_from_json_text(json.dumps(scene))
+        for mode in (0, 1):
+            with quiet_stdout():
+                fb, ni, no = rtamd.ref_render(sc, sc.width, sc.height, mode)
+            data[f"{name}/{mode}/fb"] = fb
+            data[f"{name}/{mode}/counts"] = np.array([ni, no], dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "bvh.npz"), **data)
+    print("bvh:", len(data))
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:
         for what in sys.argv[1:]:
@@ -233,3 +249,4 @@ if __name__ == "__main__":
     make_dirlights()
     make_deep()
     make_crowd()
+    make_bvh()
