@@ -105,7 +105,7 @@ def pmc_traffic(config: int, timeout: int = 120) -> dict | None:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--cpu-rows", type=int, default=64, help="rows of the 1-thread CPU-oracle band")

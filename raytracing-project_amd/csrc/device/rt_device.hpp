@@ -201,8 +201,8 @@ enum RtEvent {
     EV_COMB_GEN,       //   general sweep
     EV_LIGHT1,         // light pass 1 iterations with some lane needing a query
     EV_LIGHT2,         // light pass 2 iterations (lit lights)
-    EV_UNUSED13,       // (free slot)
-    EV_COMPACT_LEAF,   // leaf_ivl_c executions
+    EV_BOUNCE,         // trace_wave steps after the first (reflection / refraction bounces)
+    EV_COMPACT_LEAF,   // leaf_ivl_c executions (trace_wave scenes: lanes evaluating in bounce steps)
     EV_WAVES,          // waves with an active lane
     EV_COUNT
 };
@@ -226,6 +226,9 @@ struct Cnt<false> {
     }
     __device__ __forceinline__ void ev(int k) {
         if (first()) acc()[k] += 1;
+    }
+    __device__ __forceinline__ void evn(int k, unsigned n) {   // (wave-uniform n)
+        if (first()) acc()[k] += n;
     }
     __device__ __forceinline__ void pb(int) {}
     __device__ __forceinline__ void pe(int) {}
@@ -255,11 +258,13 @@ struct Cnt<false> {
     }
     __device__ __forceinline__ unsigned long long get(int k) { return acc()[k]; }
     __device__ __forceinline__ void ev(int) {}
+    __device__ __forceinline__ void evn(int, unsigned) {}
 #else
     __device__ __forceinline__ void init() {}
     __device__ __forceinline__ void pb(int) {}
     __device__ __forceinline__ void pe(int) {}
     __device__ __forceinline__ void ev(int) {}
+    __device__ __forceinline__ void evn(int, unsigned) {}
 #endif
 };
 template <>
@@ -273,6 +278,7 @@ struct Cnt<true> {
     __device__ __forceinline__ void inc(int k) { c[k] += on; }
     __device__ __forceinline__ void gate(bool b) { on = b ? 1u : 0u; }
     __device__ __forceinline__ void ev(int) {}
+    __device__ __forceinline__ void evn(int, unsigned) {}
     __device__ __forceinline__ void init() {}
     __device__ __forceinline__ void pb(int) {}
     __device__ __forceinline__ void pe(int) {}
@@ -2165,9 +2171,15 @@ __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t&
     V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));
     bool alive = true;
     const bool wave_ok = __builtin_amdgcn_read_exec() == ~0ull;
+    bool first_step = true;
     while (__any(alive)) {
         // ---- evaluate node (r, depth) on the lanes still tracing
         const bool eval = alive && depth < limit;
+        if (!first_step) {
+            cnt.ev(EV_BOUNCE);
+            cnt.evn(EV_COMPACT_LEAF, (unsigned)__builtin_popcountll(__ballot(eval)));
+        }
+        first_step = false;
         if (alive && !eval) ret = v3(RV(0.0), RV(0.0), RV(0.0));
         real ht = RV(0.0);
         DHit h;

@@ -18,7 +18,7 @@ import scenes  # noqa: E402
 
 EVENTS = ["shadow_queries", "shadow_candidates", "shadow_object_hits", "shadow_csg_hits", "primary_candidates",
           "primary_object_hits", "fold_leaves", "csg_combines", "comb_single", "comb_union_easy", "comb_general",
-          "light_pass1", "light_pass2", "(unused)", "compact_leaves", "waves"]
+          "light_pass1", "light_pass2", "bounce_steps", "compact_leaves|bounce_lanes", "waves"]
 
 
 def main():
