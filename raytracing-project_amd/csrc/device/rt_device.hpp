@@ -70,6 +70,13 @@ __device__ __forceinline__ V3 v3(real x, real y, real z) { return V3{x, y, z}; }
 __device__ __forceinline__ real dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ real dmax(real a, real b) { return (a < b) ? b : a; }   // std::max
 __device__ __forceinline__ real dmin(real a, real b) { return (b < a) ? b : a; }   // std::min
+// std::max(c, x) / std::min(c, x) with a non-NaN constant c as one v_max / v_min
+// instead of compare + two selects: equal for every x including NaN (both
+// give c); for x = -0 against c = +0 the sign of the zero may differ, so these
+// are used only where a zero result's sign cannot reach the output (each use
+// says why).
+__device__ __forceinline__ real cmax(real c, real x) { return __builtin_fmax(c, x); }
+__device__ __forceinline__ real cmin(real c, real x) { return __builtin_fmin(c, x); }
 __device__ __forceinline__ V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
 // The next representable value above x >= 0 (x itself for +inf).
 __device__ __forceinline__ double next_up(double x) {
@@ -1053,15 +1060,30 @@ __device__ __forceinline__ FRay to_fray(const DRay& r) {
     return FRay{(float)r.o.x, (float)r.o.y, (float)r.o.z, (float)r.d.x, (float)r.d.y, (float)r.d.z};
 }
 
+// The f32 cull tests work on (x, y) pairs as packed two-float vectors: on
+// gfx950 v_pk_add/mul/fma_f32 do both halves in one VALU issue, and the
+// trace kernels are VALU-issue bound.  Each half rounds exactly like the
+// scalar operation (the margins never relied on a particular order).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v f2(float x, float y) { return f2v{x, y}; }
+__device__ __forceinline__ f2v f2s(float s) { return f2v{s, s}; }
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+// |w|^2 and w.a with w = (wxy, wz)
+__device__ __forceinline__ float dot_pk(f2v axy, float az, f2v bxy, float bz) {
+    const f2v p = axy * bxy;
+    return __builtin_fmaf(az, bz, p.x + p.y);
+}
+
 __device__ __forceinline__ bool ball_touch(const float* g, const FRay& r, float t0, float t1) {
-    const float ox = r.ox - g[0], oy = r.oy - g[1], oz = r.oz - g[2];
-    const float b = ox * r.dx + oy * r.dy + oz * r.dz;
+    const f2v dxy = f2(r.dx, r.dy);
+    const f2v oxy = f2(r.ox, r.oy) - f2(g[0], g[1]);
+    const float oz = r.oz - g[2];
+    const float b = dot_pk(oxy, oz, dxy, r.dz);
     const float t = __builtin_fminf(__builtin_fmaxf(-b, t0), t1);   // closest point of the segment
-    const float qx = __builtin_fmaf(t, r.dx, ox);
-    const float qy = __builtin_fmaf(t, r.dy, oy);
+    const f2v qxy = pk_fma(f2s(t), dxy, oxy);
     const float qz = __builtin_fmaf(t, r.dz, oz);
-    const float q2 = qx * qx + qy * qy + qz * qz;
-    const float e = 4e-6f * (__builtin_fabsf(ox) + __builtin_fabsf(oy) + __builtin_fabsf(oz) + __builtin_fabsf(t) + g[3]);
+    const float q2 = dot_pk(qxy, qz, qxy, qz);
+    const float e = 4e-6f * (__builtin_fabsf(oxy.x) + __builtin_fabsf(oxy.y) + __builtin_fabsf(oz) + __builtin_fabsf(t) + g[3]);
     const float R = g[3] + e;
     return !(q2 > R * R);
 }
@@ -1494,37 +1516,66 @@ __device__ __forceinline__ float uni(float v) {
 }
 
 
-__device__ __forceinline__ bool capsule_touch(const float4 g, float ax, float ay, float az, float ux, float uy,
-                                              float uz, float uu, float rho, float mag) {
-    const float wx = g.x - ax, wy = g.y - ay, wz = g.z - az;
-    const float wu = __builtin_fmaf(wx, ux, __builtin_fmaf(wy, uy, wz * uz));
-    const float s = uu > 0.0f ? __builtin_amdgcn_fmed3f(wu * __builtin_amdgcn_rcpf(uu), 0.0f, 1.0f) : 0.0f;
-    const float qx = __builtin_fmaf(-s, ux, wx), qy = __builtin_fmaf(-s, uy, wy), qz = __builtin_fmaf(-s, uz, wz);
-    const float d2 = __builtin_fmaf(qx, qx, __builtin_fmaf(qy, qy, qz * qz));
-    const float m = 1e-5f * (mag + __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w);
-    const float R = g.w + rho + m;
+// A shadow bundle's capsule (wave-uniform): radius rho around the segment
+// [a, b], u = b - a, iuu = 1 / |u|^2 (0 for a point), m5 = 1e-5 * the
+// bundle's magnitude and rm5 = rho + m5 (the margins' uniform parts).
+struct Capsule {
+    f2v axy, bxy, uxy;
+    float az, bz, uz, iuu, rho, m5, rm5;
+    f2v abx, aby, abz;   // (a.x, b.x), ... for the half-space test
+};
+// A bundle's cone (or double cone, for lines): origins within rho of o,
+// directions within theta of a (cth = cos theta, sth = sin theta).
+struct Cone {
+    f2v oxy, axy;
+    float oz, az, cth, sth, rho, m5;
+};
+// |x| + |y| + |z| + r of a ball (the records carry it precomputed)
+__device__ __forceinline__ float ball_mag(const float4 g) {
+    return __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w;
+}
+
+__device__ __forceinline__ bool capsule_touch(const float4 g, float gmag, const Capsule& K) {
+    const f2v wxy = f2(g.x, g.y) - K.axy;
+    const float wz = g.z - K.az;
+    const float wu = dot_pk(wxy, wz, K.uxy, K.uz);
+    // (iuu = 0 for a point capsule: s = 0; a non-finite wu makes q NaN: passes)
+    const float s = __builtin_amdgcn_fmed3f(wu * K.iuu, 0.0f, 1.0f);
+    const f2v qxy = pk_fma(f2s(-s), K.uxy, wxy);
+    const float qz = __builtin_fmaf(-s, K.uz, wz);
+    const float d2 = dot_pk(qxy, qz, qxy, qz);
+    const float R = g.w + K.rho + __builtin_fmaf(1e-5f, gmag, K.m5);
     return !(d2 > R * R);   // NaN passes
 }
-__device__ __forceinline__ bool capsule_touch(const float* g, float ax, float ay, float az, float ux, float uy,
-                                              float uz, float uu, float rho, float mag) {
-    return capsule_touch(*reinterpret_cast<const float4*>(g), ax, ay, az, ux, uy, uz, uu, rho, mag);
+__device__ __forceinline__ bool capsule_touch(const float* g, const Capsule& K) {
+    const float4 b = *reinterpret_cast<const float4*>(g);
+    return capsule_touch(b, ball_mag(b), K);
 }
 
 // The same bundle seen as LINES (Primitive::interval has no range, so a CSG
 // leaf's interval is empty only if its whole line misses the leaf): every
-// lane's line lies within rho of a line through (ox, oy, oz) whose direction
-// is within theta of +-a, so a ball can be touched only if the angle between
-// w = c - o and the axis LINE is <= theta + asin(R / |w|): the double cone,
-// cone_touch with |w.a|.  Conservative in f32 like cone_touch.
-__device__ __forceinline__ bool line_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
-                                          float az, float cth, float sth, float rho, float mag) {
-    const float wx = g[0] - ox, wy = g[1] - oy, wz = g[2] - oz;
-    const float m = 1e-5f * (mag + __builtin_fabsf(g[0]) + __builtin_fabsf(g[1]) + __builtin_fabsf(g[2]) + g[3]);
-    const float R = g[3] + rho + m;
-    const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
-    const float wa = __builtin_fabsf(__builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az)));
-    const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
-    return !(L2 > R * R) | !(wa + m < rhs);   // (no branch: lanes disagree on the first test)
+// lane's line lies within rho of a line through o whose direction is within
+// theta of +-a, so a ball can be touched only if the angle between w = c - o
+// and the axis LINE is <= theta + asin(R / |w|): the double cone, cone_touch
+// with |w.a|.  Conservative in f32 like cone_touch.
+template <bool LINE>
+__device__ __forceinline__ bool cone_touch_t(const float4 g, float gmag, const Cone& K) {
+    const f2v wxy = f2(g.x, g.y) - K.oxy;
+    const float wz = g.z - K.oz;
+    const float m = __builtin_fmaf(1e-5f, gmag, K.m5);
+    const float R = g.w + K.rho + m;
+    const float L2 = dot_pk(wxy, wz, wxy, wz);
+    const float wa0 = dot_pk(wxy, wz, K.axy, K.az);
+    const float wa = LINE ? __builtin_fabsf(wa0) : wa0;
+    // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R;
+    // !(L2 > R^2): the bundle's origin region touches the ball (or NaN).  No
+    // branch: lanes disagree on the first test.
+    const float rhs = K.cth * sqrt_cull(L2 - R * R) - K.sth * R;
+    return !(L2 > R * R) | !(wa + m < rhs);
+}
+__device__ __forceinline__ bool line_touch(const float* g, const Cone& K) {
+    const float4 b = *reinterpret_cast<const float4*>(g);
+    return cone_touch_t<true>(b, ball_mag(b), K);
 }
 
 template <class CT>
@@ -1534,9 +1585,8 @@ __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
 
 // Lane j's transposed test of object j's cull record (CompiledScene::ctab)
 // against the capsule of radius rho around the segment [a, b] (u = b - a).
-__device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, float ax, float ay, float az, float bx,
-                                             float by, float bz, float ux, float uy, float uz, float uu, float rho,
-                                             float mag) {
+// Record word 5 (c1.y) is the magnitude of the record's ball or plane point.
+__device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, const Capsule& K) {
     // Lanes test objects of different types side by side, so both tests run
     // on every lane and the type selects (no divergent branches, no exec
     // bookkeeping between the record's loads and the ballot).
@@ -1544,12 +1594,11 @@ __device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, f
     // a bare half-space: the segments cross its plane only if the capsule
     // does (both axis ends farther than rho on one side: no lane); n.x - n.p
     // in f32 is within 1e-6 of the magnitudes of the signed distance, far
-    // inside the margin
-    const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
-    const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
-    const float m = rho + 1e-5f * (mag + c1.y);
-    const bool plane = !((sa > m) & (sb > m)) & !((sa < -m) & (sb < -m));   // NaN passes
-    const bool ball = capsule_touch(c0, ax, ay, az, ux, uy, uz, uu, rho, mag);
+    // inside the margin.  (sa, sb) as one packed pair.
+    const f2v sab = pk_fma(f2s(c0.x), K.abx, pk_fma(f2s(c0.y), K.aby, f2s(c0.z) * K.abz)) - f2s(c0.w);
+    const float m = __builtin_fmaf(1e-5f, c1.y, K.rm5);
+    const bool plane = !((sab.x > m) & (sab.y > m)) & !((sab.x < -m) & (sab.y < -m));   // NaN passes
+    const bool ball = capsule_touch(c0, c1.y, K);
     return (type == 1) | ((type == 2) & ball) | ((type == 3) & plane);
 }
 
@@ -1583,6 +1632,8 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
     if (!nm) return false;
     cnt.ev(EV_SHQ);
     const int f = __builtin_ctzll(nm);
+    // (the segment ends stay scalar: as packed (A, B) pairs they cost config 4
+    // 8.51 -> 8.67 ms in register moves)
     const float Ax = __builtin_fmaf(ftmin, fr.dx, fr.ox), Ay = __builtin_fmaf(ftmin, fr.dy, fr.oy),
                 Az = __builtin_fmaf(ftmin, fr.dz, fr.oz);
     const float Bx = __builtin_fmaf(ftmax, fr.dx, fr.ox), By = __builtin_fmaf(ftmax, fr.dy, fr.oy),
@@ -1599,14 +1650,21 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
     const float d = need ? __builtin_fmaxf(da, db) : 0.0f;
     const float rho = uni<UO>(cap ? sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(d)))) : 0.0f);
     const float ux = uni<UO>(bx - ax), uy = uni<UO>(by - ay), uz = uni<UO>(bz - az);
-    const float uu = uni<UO>(__builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz)));
-    const float mag = uni<UO>(__builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
-                          __builtin_fabsf(by) + __builtin_fabsf(bz) + rho + 1.0f);
+    const float uu = __builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz));
+    const float mag = __builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
+                      __builtin_fabsf(by) + __builtin_fabsf(bz) + rho + 1.0f;
+    Capsule K;
+    K.axy = f2(ax, ay), K.bxy = f2(bx, by), K.uxy = f2(ux, uy);
+    K.az = az, K.bz = bz, K.uz = uz;
+    K.iuu = uni<UO>(uu > 0.0f ? __builtin_amdgcn_rcpf(uu) : 0.0f);
+    K.rho = rho;
+    K.m5 = uni<UO>(1e-5f * mag);
+    K.rm5 = uni<UO>(rho + 1e-5f * mag);
+    K.abx = f2(ax, bx), K.aby = f2(ay, by), K.abz = f2(az, bz);
     const int lane = __lane_id();
     // line bundle for the CSG leaf masks, built on first use (cap only)
     bool lb_ready = false;
-    float lox = 0.0f, loy = 0.0f, loz = 0.0f, lax = 0.0f, lay = 0.0f, laz = 0.0f;
-    float lrho = 0.0f, lcth = -1.0f, lsth = 1.0f, lmag = 0.0f;
+    Cone LB{f2(0.0f, 0.0f), f2(0.0f, 0.0f), 0.0f, 0.0f, -1.0f, 1.0f, 0.0f, 0.0f};
     bool hit = false;
     const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
     uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 some querying segment can reach
@@ -1616,7 +1674,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
                 const int c = ch + lane;
                 const int cr = c < nch ? c : nch - 1;
                 const float4 k0 = S.wchunk[2 * cr], k1 = S.wchunk[2 * cr + 1];
-                const bool pass = (c < nch) & record_touch(k0, k1, ax, ay, az, bx, by, bz, ux, uy, uz, uu, rho, mag);
+                const bool pass = (c < nch) & record_touch(k0, k1, K);
                 cm = (cap && exec_full()) ? __ballot(pass) : ~0ull;
             }
             if (!((cm >> (ch & 63)) & 1ull)) continue;
@@ -1629,7 +1687,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
         const int jr = j < S.n_objs ? j : S.n_objs - 1;
         const float4 c0 = S.ctab[2 * jr], c1 = S.ctab[2 * jr + 1];
         const bool pass = (j < S.n_objs) &
-                          (cap ? record_touch(c0, c1, ax, ay, az, bx, by, bz, ux, uy, uz, uu, rho, mag)
+                          (cap ? record_touch(c0, c1, K)
                                : __float_as_int(c1.x) != 0);
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
@@ -1662,7 +1720,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
             if (cap && ob.npb > 0 && exec_full()) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
                 const bool in = lane < ob.npb;
-                if (!__any(in && capsule_touch(g, ax, ay, az, ux, uy, uz, uu, rho, mag))) {
+                if (!__any(in && capsule_touch(g, K))) {
                     if (need) cnt.inc(RT_OPC_CULLED);
                     cnt.pe(PH_OBJ_PREF);
                     continue;
@@ -1670,26 +1728,29 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
                 if (!lb_ready) {
                     // line bundle of the querying lanes (lane f's line as the axis)
                     lb_ready = true;
-                    lox = rdlane_f(fr.ox, f), loy = rdlane_f(fr.oy, f), loz = rdlane_f(fr.oz, f);
-                    lax = rdlane_f(fr.dx, f), lay = rdlane_f(fr.dy, f), laz = rdlane_f(fr.dz, f);
+                    const float lox = rdlane_f(fr.ox, f), loy = rdlane_f(fr.oy, f), loz = rdlane_f(fr.oz, f);
+                    const float lax = rdlane_f(fr.dx, f), lay = rdlane_f(fr.dy, f), laz = rdlane_f(fr.dz, f);
                     const float dxo = fr.ox - lox, dyo = fr.oy - loy, dzo = fr.oz - loz;
                     const float do2 = need ? dxo * dxo + dyo * dyo + dzo * dzo : 0.0f;
                     const float dc = need ? __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, lax, __builtin_fmaf(fr.dy, lay, fr.dz * laz)))
                                           : 0.0f;
-                    lrho = uni<UO>(sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(do2)))));
+                    const float lrho = uni<UO>(sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(do2)))));
                     const float dcm = __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f;
-                    lcth = uni<UO>(1.0f - dcm);
-                    lsth = uni<UO>(sqrt_cull(__builtin_fmaxf(0.0f, 1.0f - lcth * lcth)) + 1e-6f);
-                    lmag = uni<UO>(__builtin_fabsf(lox) + __builtin_fabsf(loy) + __builtin_fabsf(loz) + lrho + 1.0f);
+                    const float lcth = uni<UO>(1.0f - dcm);
+                    LB.oxy = f2(lox, loy), LB.axy = f2(lax, lay), LB.oz = loz, LB.az = laz;
+                    LB.cth = lcth;
+                    LB.sth = uni<UO>(sqrt_cull(__builtin_fmaxf(0.0f, 1.0f - lcth * lcth)) + 1e-6f);
+                    LB.rho = lrho;
+                    LB.m5 = uni<UO>(1e-5f * (__builtin_fabsf(lox) + __builtin_fabsf(loy) + __builtin_fabsf(loz) + lrho + 1.0f));
                 }
 #ifdef RT_NO_LEAF_MASK
                 use_mask = false;
 #else
-                use_mask = lcth > 0.0f;
+                use_mask = LB.cth > 0.0f;
 #endif
                 if (use_mask) {
                     const bool full = exec_full();
-                    const uint64_t b = __ballot(in && line_touch(g, lox, loy, loz, lax, lay, laz, lcth, lsth, lrho, lmag));
+                    const uint64_t b = __ballot(in && line_touch(g, LB));
                     lmask = full ? b : ~0ull;
                 }
             }
@@ -1746,22 +1807,12 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
 // over those, in scene order, exactly as scene_intersect (ties and the
 // shrinking closest-so-far included).  Conservative in f32 like
 // capsule_touch: results are unchanged.
-__device__ __forceinline__ bool cone_touch(const float4 g, float ox, float oy, float oz, float ax, float ay,
-                                          float az, float cth, float sth, float rho, float mag) {
-    const float wx = g.x - ox, wy = g.y - oy, wz = g.z - oz;
-    const float m = 1e-5f * (mag + __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w);
-    const float R = g.w + rho + m;
-    const float L2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
-    const float wa = __builtin_fmaf(wx, ax, __builtin_fmaf(wy, ay, wz * az));
-    // angle(w, a) <= theta + asin(R / |w|)  <=>  w.a >= cos(theta) sqrt(L2 - R^2) - sin(theta) R;
-    // !(L2 > R^2): the bundle's origin region touches the ball (or NaN).  No
-    // branch: lanes disagree on the first test.
-    const float rhs = cth * sqrt_cull(L2 - R * R) - sth * R;
-    return !(L2 > R * R) | !(wa + m < rhs);
+__device__ __forceinline__ bool cone_touch(const float4 g, float gmag, const Cone& K) {
+    return cone_touch_t<false>(g, gmag, K);
 }
-__device__ __forceinline__ bool cone_touch(const float* g, float ox, float oy, float oz, float ax, float ay,
-                                          float az, float cth, float sth, float rho, float mag) {
-    return cone_touch(*reinterpret_cast<const float4*>(g), ox, oy, oz, ax, ay, az, cth, sth, rho, mag);
+__device__ __forceinline__ bool cone_touch(const float* g, const Cone& K) {
+    const float4 b = *reinterpret_cast<const float4*>(g);
+    return cone_touch_t<false>(b, ball_mag(b), K);
 }
 
 //
@@ -1805,6 +1856,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     const bool wide = !(cth > 0.0f);   // a bundle wider than 90 degrees (or no cone): no culling
     const float sth = sqrt_cull(__builtin_fmaxf(0.0f, 1.0f - cth * cth)) + 1e-6f;
     const float mag = __builtin_fabsf(ox) + __builtin_fabsf(oy) + __builtin_fabsf(oz) + rho + 1.0f;
+    const Cone K{f2(ox, oy), f2(ax, ay), oz, az, cth, sth, rho, 1e-5f * mag};
     const int lane = __lane_id();
     real closest = tmax;
     int win = -1;
@@ -1823,7 +1875,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 const int cr = c < nch ? c : nch - 1;
                 const float4 k0 = S.wchunk[2 * cr], k1 = S.wchunk[2 * cr + 1];
                 const int ktype = __float_as_int(k1.x);
-                const bool pass = (c < nch) & ((ktype != 2) | wide | cone_touch(k0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+                const bool pass = (c < nch) & ((ktype != 2) | wide | cone_touch(k0, k1.y, K));
                 cm = (cone && exec_full()) ? __ballot(pass) : ~0ull;
             }
             if (!((cm >> (ch & 63)) & 1ull)) continue;
@@ -1834,7 +1886,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
         const float4 c0 = S.ctab[2 * jr], c1 = S.ctab[2 * jr + 1];
         const int type = __float_as_int(c1.x);
         const bool pass = (j < S.n_objs) & (type != 0) &
-                          ((type != 2) | wide | cone_touch(c0, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+                          ((type != 2) | wide | cone_touch(c0, c1.y, K));
         const int nc = S.n_objs - base;
         uint64_t m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
@@ -1858,7 +1910,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             uint64_t lmask = ~0ull;
 #ifdef RT_NO_LEAF_MASK
             const bool use_mask = false;
-            if (!wide && ob.npb > 0 && exec_full() && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
+            if (!wide && ob.npb > 0 && exec_full() && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), K))) {
                 if (valid) cnt.inc(RT_OPC_CULLED);
                 cnt.pe(PH_OBJ_PREF);
                 continue;
@@ -1869,13 +1921,13 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             if (use_mask) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
                 const bool in = lane < ob.npb;
-                if (!__any(in && cone_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag))) {
+                if (!__any(in && cone_touch(g, K))) {
                     if (valid) cnt.inc(RT_OPC_CULLED);
                     cnt.pe(PH_OBJ_PREF);
                     continue;
                 }
                 const bool full = exec_full();
-                const uint64_t b = __ballot(in && line_touch(g, ox, oy, oz, ax, ay, az, cth, sth, rho, mag));
+                const uint64_t b = __ballot(in && line_touch(g, K));
                 lmask = full ? b : ~0ull;
             }
             if (S.cull && ob.has_bound && !__any(valid && ball_touch(ob.fb, fr, ftmin, (float)closest))) {
@@ -2004,7 +2056,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
     // objects, culling on): the capsule test needs every lane active
     const bool wave_full = WV && __builtin_amdgcn_read_exec() == ~0ull;
     const V3 n = hit.n;
-    const real eps = dmax(RV(1e-3), RV(1e-4) * ht);
+    const real eps = cmax(RV(1e-3), RV(1e-4) * ht);   // (no zeros)
     // Two passes over the lights so that only (p, n, eps) stay live across
     // the shadow queries (register pressure): pass 1 decides, per light, the
     // reference's early-outs and the occlusion query; pass 2 recomputes the
@@ -2065,7 +2117,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 c[2 * kPoolThreads] = wi.z;
                 c[3 * kPoolThreads] = dist;
             }
-            const real ndotl = dmax(RV(0.0), dot3(n, wi));
+            const real ndotl = cmax(RV(0.0), dot3(n, wi));   // (only compared with 0)
             const real max_t = dist - eps;
             // shading.cpp:86-103: back-facing lights and lights closer than
             // the shadow epsilon are skipped before the occlusion query
@@ -2117,9 +2169,9 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 const auto wq = div3(tl.x, tl.y, tl.z, dist);
                 wi = v3(wq.x, wq.y, wq.z);
             }
-            const real ndotl = dmax(RV(0.0), dot3(n, wi));
+            const real ndotl = cmax(RV(0.0), dot3(n, wi));   // (> 0: a lit light)
             cnt.inc(RT_OPC_SHADE_LIGHT);
-            const real ed = dmax(RV(0.5), dist);
+            const real ed = cmax(RV(0.5), dist);
             const real falloff = RV(1.0) / (ed * ed);
             const real f2 = falloff * RV(2.0);
             const V3 IL = v3(L->intensity[0] * f2, L->intensity[1] * f2, L->intensity[2] * f2);
@@ -2130,17 +2182,17 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 cnt.inc(RT_OPC_SHADE_SPEC);
                 const V3 rr = normalized(v3(RV(2.0) * dot3(n, wi) * n.x - wi.x, RV(2.0) * dot3(n, wi) * n.y - wi.y,
                                             RV(2.0) * dot3(n, wi) * n.z - wi.z));
-                const real rdotv = dmax(RV(0.0), dot3(rr, wo));
-                const real spec = pow_spec(rdotv, shin) * ks;
+                const real rdotv = cmax(RV(0.0), dot3(rr, wo));
+                const real spec = pow_spec(rdotv, shin) * ks;   // (a -0 here gives Es = -0: combine ignores the sign)
                 Es = v3(IL.x * spec, IL.y * spec, IL.z * spec);
             }
             E = combine(E, combine(Ed, Es));
         }
     }
     if (WV) cnt.pe(PH_SHADE2);
-    E.x = dmin(RV(1.5), E.x);
-    E.y = dmin(RV(1.5), E.y);
-    E.z = dmin(RV(1.5), E.z);
+    E.x = cmin(RV(1.5), E.x);   // (keeps a zero's sign)
+    E.y = cmin(RV(1.5), E.y);
+    E.z = cmin(RV(1.5), E.z);
     return has_mat ? E : v3(RV(1.0), RV(0.0), RV(1.0));   // magenta for a null material (shading.cpp:33)
 }
 

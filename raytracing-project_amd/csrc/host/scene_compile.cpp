@@ -60,6 +60,14 @@ void float_ball(const double c[3], double r, float out[4]) {
     out[3] = std::nextafter((float)(r + 1e-6 * (1.0 + mag)), INFINITY);
 }
 
+// |x| + |y| + |z| + r of a float ball, rounded up: the magnitude a cull record
+// carries (record word 5) for the device tests' margins, so the transposed
+// tests do not re-add it per lane.
+float float_ball_mag(const float b[4]) {
+    const double m = std::fabs((double)b[0]) + std::fabs((double)b[1]) + std::fabs((double)b[2]) + (double)b[3];
+    return std::nextafter((float)m, INFINITY);
+}
+
 bool is_degenerate_scaling(const rt_node& n) {
     const double kEPS = 1e-6;   // core.h:10, checked at transform.cpp:97
     return n.kind == RT_NODE_SCALING &&
@@ -450,6 +458,7 @@ public:
             } else if (o.has_bound) {
                 type = 2;
                 for (int k = 0; k < 4; ++k) c[k] = o.fb[k];
+                c[5] = float_ball_mag(c);
             } else if (o.kind == OBJ_HALF) {
                 type = 3;
                 const double* v = d_.nodes[o.node].v;   // point v[0..2], unit normal v[3..5]
@@ -548,6 +557,7 @@ public:
                 const double mag = std::fabs(C[0]) + std::fabs(C[1]) + std::fabs(C[2]) + R;
                 R = R * (1.0 + 1e-7) + 1e-7 * (1.0 + mag);
                 float_ball(C, R, rec);
+                rec[5] = float_ball_mag(rec);
                 type = 2;
             }
             std::memcpy(&rec[4], &type, sizeof(int));
