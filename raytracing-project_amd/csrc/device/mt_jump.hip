@@ -529,18 +529,28 @@ hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
     release();
     locate_poly_file();
     std::vector<uint32_t> polys = mt_tree_polys(K_blocks, levels_needed);
-    std::vector<uint16_t> taps;
+    // the set coefficients of every polynomial, in order (~2.3 M taps for 4
+    // levels): sized by popcount, then one ctz walk per word (a bit-by-bit
+    // scan took ~40 ms of the CLI's one-time setup)
+    const size_t n_poly = (size_t)levels_needed * (kMTRadix - 1);
+    size_t n_taps = 0;
+    for (size_t k = 0; k < n_poly * kPolyWords32; ++k) n_taps += (size_t)__builtin_popcount(polys[k]);
+    std::vector<uint16_t> taps(n_taps + 8, 0);
+    size_t o = 0;
     off.assign(1, 0);
     for (int j = 0; j < levels_needed; ++j)
         for (int m = 0; m < kMTRadix; ++m) {
             if (m > 0) {
                 const uint32_t* P = polys.data() + ((size_t)j * (kMTRadix - 1) + (m - 1)) * kPolyWords32;
-                for (int i = 0; i < kMTDeg; ++i)
-                    if ((P[i >> 5] >> (i & 31)) & 1u) taps.push_back((uint16_t)i);
+                for (int w = 0; w < kPolyWords32; ++w)
+                    for (uint32_t b = P[w]; b; b &= b - 1) {
+                        const int i = w * 32 + __builtin_ctz(b);
+                        if (i < kMTDeg) taps[o++] = (uint16_t)i;
+                    }
             }
-            off.push_back((int32_t)taps.size());
+            off.push_back((int32_t)o);
         }
-    taps.resize(taps.size() + 8, 0);
+    taps.resize(o + 8, 0);
     uint32_t win[kMTN];
     mt_first_window(12345u, win);
     hipError_t e = hipMalloc(&d_taps, taps.size() * sizeof(uint16_t));
