@@ -2043,7 +2043,10 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 // never populates directional lights).
 // DL: the scene may have directional lights (the lean kernels, chosen only
 // for scenes without, do not carry their code or registers).
-template <bool EAGER, bool DEEP, bool DL, int WV, bool UO = false, class CT>
+#ifndef RT_STD_UO
+#define RT_STD_UO false
+#endif
+template <bool EAGER, bool DEEP, bool DL, int WV, bool UO = RT_STD_UO, class CT>
 __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt,
                     bool valid = true) {
     // valid = false: a lane of the wave that has nothing to shade (a primary

@@ -29,7 +29,10 @@ def main(src):
             m["fetch_bytes_x2"] = 2.0 * m["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in m:
             m["write_bytes"] = m["WRITE_SIZE"] * 1024
-        short = name.split("(")[0][-70:]
+        # the name up to its argument list ("(anonymous namespace)" is part of
+        # the qualified name, not the argument list)
+        base = name.replace("(anonymous namespace)", "{anon}")
+        short = base.split("(")[0].replace("{anon}", "(anonymous namespace)")[-70:]
         out[short] = {k: round(v, 3) for k, v in m.items()}
     json.dump(out, open(os.path.join(src, "summary.json"), "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
