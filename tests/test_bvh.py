@@ -105,6 +105,12 @@ def test_wave_bvh_structure(rt, name):
         m = b["wctab"][mem, :4].astype(np.float64)
         reach = np.linalg.norm(m[:, :3] - cc, axis=1) + m[:, 3]
         assert np.all(reach <= rc * (1 + 1e-6)), (c, float(reach.max()), rc)
+    # ball records (objects and chunks) carry |x| + |y| + |z| + r in word 5,
+    # rounded up, for the device tests' margins (rt_device.hpp record_touch)
+    for rec, typ in ((b["wctab"], t), (b["wchunk"], b["ctype"])):
+        balls = rec[typ == 2].astype(np.float64)
+        mag = np.abs(balls[:, :3]).sum(axis=1) + balls[:, 3]
+        assert np.all(balls[:, 5] >= mag) and np.all(balls[:, 5] <= mag * (1 + 1e-6))
 
 
 def test_small_scenes_have_no_bvh(rt):
