@@ -1497,12 +1497,6 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {   // every lane m
     v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false));
     v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false));
     v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false));
-#ifdef RT_EXP_BCAST_MAX
-    // row_bcast:15 / row_bcast:31 carry each row's maximum into the next rows; lane 63 ends with all
-    v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
-    v = umax32(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-#endif
     const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
     const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
     return umax32(umax32(r0, r1), umax32(r2, r3));
