@@ -102,9 +102,88 @@ def pmc_traffic(config: int, timeout: int = 120) -> dict | None:
     return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write}
 
 
+def host_cpu() -> dict:
+    """The CPU the baseline ran on (report nproc and the model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"model": model or platform.processor() or platform.machine(), "nproc": os.cpu_count(),
+            "usable_cpus": usable,
+            "note": "nproc counts the whole machine; the GPU box grants this job 16 of them (OMP_NUM_THREADS)"}
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    script (one per GPU, LOCAL_RANK = GPU index) with the environment
+    torch.distributed.run would give them, BEFORE this process makes any HIP
+    call (it never makes one), and exit with their status.  Rank 0 prints the
+    JSON line; the others print nothing on stdout.  If a rank fails, the
+    others are stopped (they would wait in a collective for it)."""
+    import uuid
+
+    port = str(_free_port())
+    run_id = uuid.uuid4().hex[:12]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RTAMD_RUN_ID=run_id,
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(range(n))
+        while live:
+            time.sleep(0.05)
+            for r in list(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.remove(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr,
+                          flush=True)
+                    for q in live:
+                        procs[q].terminate()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        try:   # the id file, if rank 0 did not get to remove it
+            os.unlink(os.path.join(tempfile.gettempdir(), f"rtamd_uid_{port}_{run_id}"))
+        except FileNotFoundError:
+            pass
+    return rc
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Without a launcher's RANK/WORLD_SIZE, bench.py starts them itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up ranks and the id exchange, print each rank's view, stop before any GPU call")
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=4)
@@ -117,17 +196,34 @@ def main() -> int:
                     help="time the NON-PARITY FP32 fast path as the headline (RT_FLAG_FP32); default is FP64")
     ap.add_argument("--fp32-steps", type=int, default=20, help="frames of the FP32 side leg (0 = skip)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    import rendezvous
+
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    rank, world, local = rendezvous.env_ranks()
+    if world != args.gpus:
+        # never print a line whose n_gpus is not the --gpus asked for
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+
+    if args.dry_run:
+        got = rendezvous.share_bytes(rank, bytes(range(128)) if rank == 0 else None, 128) if world > 1 else b""
+        print(json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local,
+                          "id_ok": world == 1 or got == bytes(range(128))}), flush=True)
+        return 0
 
     import numpy as np  # noqa: F401
 
-    import rendezvous
     import rtamd
     import scenes
 
     # No torch here: librtamd.so brings its own HIP runtime (/opt/rocm's, the
     # one `ray` uses) and does the collectives over RCCL itself; a second,
     # torch-bundled runtime in the same process is refused (rtamd.amd_lib).
-    rank, world, local = rendezvous.env_ranks()
     lib = rtamd.amd_lib()
     rtamd.set_device(local)
 
@@ -149,7 +245,8 @@ def main() -> int:
     if lib.rt_dist_create(uid, world, rank, C.byref(dh)) != 0:
         raise RuntimeError(f"rt_dist_create failed: {rtamd.last_error()}")
     if world > 1:
-        lib.rt_dist_barrier(dh)   # every rank holds the communicator: the id file can go
+        if lib.rt_dist_barrier(dh) != 0:   # every rank holds the communicator: the id file can go
+            raise RuntimeError(f"rt_dist_barrier failed: {rtamd.last_error()}")
         rendezvous.cleanup(rank)
 
     def reduce_max(vals):
@@ -169,7 +266,7 @@ def main() -> int:
         if lib.rt_dist_barrier(dh) != 0:
             raise RuntimeError(f"rt_dist_barrier failed: {rtamd.last_error()}")
 
-    n_rows = len(rtamd.dist_rows(H, world, rank))
+    n_rows = len(rtamd.dist_rows(H, world, rank, mode))
     frame = rtamd.DeviceBuffer(H * W * 3 * 8) if rank == 0 else None
     frame_ptr = frame.ptr if frame is not None else None
     stream = rtamd.Stream()
@@ -341,7 +438,8 @@ def main() -> int:
         raysm = ostm.rays_intersect + ostm.rays_occluded
         cpu = {"value": round(raysm / dtm / 1e6, 4), "unit": "Mrays/s", "cores": nt, "kind": "port",
                "sample": f"whole config-{args.config} frame {W}x{H}: {raysm} rays in {dtm:.1f} s on {nt} threads "
-                         f"(oracle/oracle.c, rows split across threads; {platform.machine()} host)"}
+                         f"(oracle/oracle.c, rows split across threads; {platform.machine()} host)",
+               "host": host_cpu()}
         # faithful to the reference: one thread, a band through the middle of the frame
         r0 = max(0, H // 2 - args.cpu_rows // 2)
         r1 = min(H, r0 + args.cpu_rows)
@@ -380,8 +478,8 @@ def main() -> int:
         "data": "synthetic: reference example scene JSON + mt19937(12345) jitter, rendered on device",
         "config": {"workload": name, "width": W, "height": H, "mode": "paper" if mode else "standard",
                    "rays_per_frame": int(rays_per_frame), "rays_traced_per_frame": int(traced_total / args.steps),
-                   "parallelism": f"row-strips8x{world}" + (", RCCL ncclGather to rank 0 in 4 chunks" if world > 1
-                                                            else ""),
+                   "parallelism": f"{world} ranks, 1 GPU each: row-strips{30 if mode == 1 else 8}x{world}" +
+                                  (", RCCL ncclGather to rank 0 in 4 chunks" if world > 1 else ""),
                    "cull": not args.no_cull},
         "roofline": {"bound": "fp64-valu", "achieved": round(achieved, 3), "peak": FP64_VALU_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP64_VALU_PEAK_TFLOPS, 4),

@@ -45,12 +45,14 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4   /* 2: rt_scene_desc gained directional lights
+#define RT_ABI_VERSION 5   /* 2: rt_scene_desc gained directional lights
                               3: rt_stats gained the output-path timings; multi-GPU
                                  and device-output entry points (rt_render_multi,
                                  rt_render_rgb8, rt_dist_*)
                               4: rt_shutdown, device-buffer utilities, rt_dist_reduce_max /
-                                 rt_dist_barrier */
+                                 rt_dist_barrier
+                              5: rt_dist_set_timeout, per-frame rank agreement,
+                                 rt_host_register / rt_host_unregister */
 
 /* ---------------------------------------------------------------- errors */
 enum rt_status {
@@ -282,6 +284,20 @@ int rt_render_dist_rgb8(rt_dist* d, const rt_scene* s, int W, int H, int mode, i
  * ranks timing). */
 int rt_dist_reduce_max(rt_dist* d, double* vals_host, int n);
 int rt_dist_barrier(rt_dist* d);
+/* Failure behaviour of rt_render_dist[_rgb8] with more than one rank.  Every
+ * rank issues every collective of a frame whatever happens locally, and the
+ * ranks agree twice per frame through small RCCL max-reductions: before the
+ * first gather on the frame descriptor (W, H, mode, output kind, flags) and
+ * on each rank's setup status; before the last gather on each rank's trace
+ * status.  So a rank-local failure makes EVERY rank return an error (the
+ * failing rank its own; the others RT_ERR_INVALID_ARG for a descriptor
+ * mismatch, RT_ERR_HIP naming the failed ranks otherwise) and the next frame
+ * renders normally.  A wait for peers that exceeds the rank's timeout (or an
+ * RCCL asynchronous error) aborts the communicator (ncclCommAbort) and returns
+ * RT_ERR_HIP; that handle then refuses frames and must be destroyed.  The
+ * timeout is RT_DIST_TIMEOUT_MS from the environment at creation (default
+ * 120000) or rt_dist_set_timeout. */
+int rt_dist_set_timeout(rt_dist* d, int timeout_ms);
 /* The partition: writes the output rows of `rank` (ascending) to rows_out
  * (room for H entries) and returns their count; <0 on bad arguments.
  * rt_dist_rows is the standard-mode partition (RT_STRIP_ROWS); paper mode
@@ -348,6 +364,12 @@ int rt_memcpy_d2h(void* host, const void* dev, size_t bytes);
 int rt_device_synchronize(void);
 int rt_stream_create(void** stream_out);             /* non-blocking HIP stream              */
 int rt_stream_destroy(void* stream);
+/* Page-lock an existing host buffer (hipHostRegister) so that the output
+ * copies of rt_render_rgb8 / rt_render_multi into it run as direct DMA
+ * instead of through the runtime's pageable staging (the `ray` CLI registers
+ * its output buffer while HIP starts).  Unregister before freeing it. */
+int rt_host_register(void* host, size_t bytes);
+int rt_host_unregister(void* host);
 /* One-time setup costs of this process so far, host wall clock in ms:
  * out[0] scene compile + upload (first frame of each scene), out[1] jitter
  * checkpoint-table builds / extensions, out[2] first trace-kernel launch

@@ -79,6 +79,16 @@ int rt_test_render_dist_sim(const struct rt_scene* s, int W, int H, int mode, in
  * Free with rt_dist_destroy. */
 struct rt_dist;
 int rt_test_dist_create_rccl1(struct rt_dist** out);
+/* Fault injection on the next frame of d (rt_render_dist): 1 = this rank's
+ * trace fails at its middle chunk, 2 = the collective stream is held past the
+ * rank's timeout (bounded: the holding kernel always ends). */
+int rt_test_dist_inject(struct rt_dist* d, int what);
+/* GPU: one simulated rank (rank of world) of a distributed frame on the
+ * current device through the product's rank path, the RCCL gather replaced by
+ * a device copy (rank 0 also places every slot).  Ranks are cached, so a
+ * repeated call times a warm rank.  For per-rank timing (tools/sim_ranks.py). */
+int rt_test_dist_sim_rank(const struct rt_scene* s, int W, int H, int mode, int flags, int world, int rank, int rgb8,
+                          struct rt_stats* stats);
 
 #ifdef __cplusplus
 }

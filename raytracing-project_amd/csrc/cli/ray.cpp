@@ -78,12 +78,17 @@ int main(int argc, char** argv) {
             if (!done) (void)rt_shutdown();
         }
     } teardown;
-    // the output bytes are written by the device path into this buffer; its
-    // pages are touched here, on a helper thread, while the main thread
-    // initialises HIP (page faults of a fresh 25 MB buffer otherwise land on
-    // the D2H copy)
+    // the output bytes are written by the device path into this buffer; on a
+    // helper thread, while the main thread initialises HIP, its pages are
+    // touched and then page-locked (rt_host_register), so the one D2H copy runs
+    // as direct DMA instead of through the runtime's pageable staging (the
+    // process's first large pageable copy: ~10 ms for 25 MB)
     std::vector<uint8_t> rgb;
-    std::thread prefault([&rgb, W, H] { rgb.assign((size_t)W * H * 3, 0); });
+    bool registered = false;
+    std::thread prefault([&rgb, &registered, W, H] {
+        rgb.assign((size_t)W * H * 3, 0);
+        registered = rt_host_register(rgb.data(), rgb.size()) == RT_OK;
+    });
     // HIP runtime initialisation (the first HIP call of the process), timed on its own for --stats
     const auto t_hip0 = std::chrono::steady_clock::now();
     (void)rt_device_count();
@@ -106,6 +111,7 @@ int main(int argc, char** argv) {
         return 4;
     }
     const auto t2 = std::chrono::steady_clock::now();
+    if (registered) (void)rt_host_unregister(rgb.data());
     teardown.done = true;
     (void)rt_shutdown();
     const auto t3 = std::chrono::steady_clock::now();

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -34,6 +36,7 @@
 
 #include "rt.h"
 #include "rt_internal.hpp"
+#include "rt_launch.hpp"
 #include "rt_test.h"
 
 namespace {
@@ -156,6 +159,46 @@ hipError_t place_rows(const void* src, const int32_t* rows_dev, int n_slots, siz
     return launch(uint8_t{});
 }
 
+// Paper-mode distributed frames gather one paper-code byte per pixel
+// (rtamd::paper_code_value): gathered slot i (W codes) -> row rows[i] of dst,
+// decoded to FP64 RGB (kind 0) or to toByte'd RGB8 (kind 1, core.h:313-316).
+template <bool RGB8>
+__global__ void k_place_codes(const uint8_t* __restrict__ src, const int32_t* __restrict__ rows, int n_slots, int W,
+                              void* __restrict__ dst) {
+    const size_t total = (size_t)W * n_slots;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t slot = i / W, x = i - slot * W;
+        const int32_t d = rows[slot];
+        if (d < 0) continue;
+        const double v = rtamd::paper_code_value(src[i]);
+        const size_t o = ((size_t)d * W + x) * 3;
+        if constexpr (RGB8) {
+            double c = (v < 1.0) ? v : 1.0;
+            c = (0.0 < c) ? c : 0.0;
+            const uint8_t b = (uint8_t)(int)round(c * 255.0);
+            uint8_t* q = static_cast<uint8_t*>(dst) + o;
+            q[0] = b;
+            q[1] = b;
+            q[2] = b;
+        } else {
+            double* q = static_cast<double*>(dst) + o;
+            q[0] = v;
+            q[1] = v;
+            q[2] = v;
+        }
+    }
+}
+
+hipError_t place_codes(const uint8_t* src, const int32_t* rows_dev, int n_slots, int W, int kind, void* dst,
+                       hipStream_t st) {
+    if (n_slots <= 0) return hipSuccess;
+    const size_t total = (size_t)W * n_slots;
+    const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 16384);
+    if (kind) hipLaunchKernelGGL(k_place_codes<true>, dim3(blocks), dim3(256), 0, st, src, rows_dev, n_slots, W, dst);
+    else hipLaunchKernelGGL(k_place_codes<false>, dim3(blocks), dim3(256), 0, st, src, rows_dev, n_slots, W, dst);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 // One rank of a frame distribution (also the single-device case, world 1).
@@ -175,6 +218,17 @@ struct rt_dist {
     DevBuf* sim_stage = nullptr;              // rt_test_render_dist_sim: shared stage, copies instead of RCCL
     bool force_collective = false;            // rt_test_dist_create_rccl1: world 1 through ncclGather
     DevBuf red;                               // rt_dist_reduce_max scratch
+    // Per-frame agreement (collective frames): the frame descriptor + each
+    // rank's setup status before the first gather, each rank's trace status
+    // before the last one (int64 slots, ncclMax), read back through pinned
+    // host memory.
+    DevBuf xchg;
+    int64_t* xchg_host = nullptr;
+    hipEvent_t ev_desc = nullptr;
+    bool dead = false;                        // communicator aborted: the handle renders no more frames
+    std::string dead_why;
+    double timeout_ms = 120000.0;             // RT_DIST_TIMEOUT_MS / rt_dist_set_timeout
+    int inject = 0;                           // rt_test_dist_inject (next frame only)
     bool collective() const { return world > 1 || force_collective; }
 };
 
@@ -191,7 +245,99 @@ int dist_init_streams(rt_dist& D) {
     for (auto& e : D.ev_gs) HIP_TRY(hipEventCreate(&e));
     for (auto& e : D.ev_ge) HIP_TRY(hipEventCreate(&e));
     HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&D.ev_desc, hipEventDisableTiming));
     return RT_OK;
+}
+
+// ------------------------------------------------ frame agreement + waits
+// A rank that fails on its own (a launch error, an allocation, a bad frame
+// argument) must not leave its peers blocked in a collective it never joins.
+// So every rank of a collective frame issues every collective of the frame
+// whatever happened locally, and the ranks agree on the outcome through two
+// small max-reductions of int64 slots on the collective stream:
+//   before the first gather: the frame descriptor (W, H, mode, kind, flags as
+//     v and -v: all ranks equal iff max(v) == v and max(-v) == -v) and one
+//     setup-failure slot per rank.  The host waits for it while the first
+//     chunk traces; on a mismatch or a failure no rank issues a gather;
+//   before the last gather: one trace-failure slot per rank (the last chunk
+//     traces meanwhile), read back after the frame.
+// Waits on the collective stream poll with a deadline and the communicator's
+// asynchronous error; on either the communicator is aborted (ncclCommAbort)
+// and the handle refuses further frames: a rank whose peer died returns
+// RT_ERR_HIP instead of hanging.
+constexpr int kDescFields = 5;
+size_t xchg_slots(int world) { return 2 * kDescFields + 2 * (size_t)world; }
+
+int dist_init_xchg(rt_dist& D) {
+    const size_t bytes = xchg_slots(D.world) * sizeof(int64_t);
+    HIP_TRY(D.xchg.ensure(bytes));
+    if (!D.xchg_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&D.xchg_host), bytes, hipHostMallocDefault));
+    return RT_OK;
+}
+
+void dist_abort(rt_dist& D, const std::string& why) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (D.comm && D.own_comm) (void)ncclCommAbort(D.comm);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    D.comm = nullptr;
+    D.own_comm = false;
+    D.dead = true;
+    char buf[64];
+    std::snprintf(buf, sizeof buf, " [ncclCommAbort %.1f ms]", ms);
+    D.dead_why = why + buf;
+}
+
+int dist_wait(rt_dist& D, hipEvent_t ev, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return RT_OK;
+        if (q != hipErrorNotReady) {
+            rtamd::set_last_error(std::string("rt_render_dist: ") + what + ": " + hipGetErrorString(q));
+            return RT_ERR_HIP;
+        }
+        if (D.comm) {
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(D.comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                const std::string why = std::string("RCCL asynchronous error during ") + what + ": " +
+                                        ncclGetErrorString(ae);
+                dist_abort(D, why);
+                rtamd::set_last_error("rt_render_dist: " + why + " (communicator aborted)");
+                return RT_ERR_HIP;
+            }
+        }
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > D.timeout_ms) {
+            const std::string why = std::string("timed out after ") + std::to_string((long)D.timeout_ms) +
+                                    " ms waiting for " + what + " (a peer rank did not take part)";
+            dist_abort(D, why);
+            rtamd::set_last_error("rt_render_dist: " + why + "; communicator aborted");
+            return RT_ERR_HIP;
+        }
+        if (it < 4096) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+// rt_test_dist_inject: a kernel that holds the collective stream for a bounded
+// time (every wave leaves after max_ticks of the 100 MHz wall clock), standing
+// in for a peer that never arrives.
+__global__ void k_test_stall(unsigned long long max_ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < max_ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+enum { kInjectTraceFail = 1, kInjectStall = 2 };
+
+// RT_DIST_TIMEOUT_MS: how long a rank waits for its peers inside one frame
+// before it aborts the communicator (default 120 s).
+double env_timeout_ms() {
+    const char* e = std::getenv("RT_DIST_TIMEOUT_MS");
+    if (e && *e) {
+        const double v = std::atof(e);
+        if (v > 0) return v;
+    }
+    return 120000.0;
 }
 
 // One rank's part of a frame.  kind 0: FP64 frame (W*H*3 doubles); kind 1:
@@ -201,27 +347,61 @@ int dist_init_streams(rt_dist& D) {
 int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags, int kind, void* out_root,
                hipStream_t st, rt_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
-    if (!s) { rtamd::set_last_error("rt_render_dist: scene is NULL"); return RT_ERR_INVALID_ARG; }
-    if (W <= 0 || H <= 0) { rtamd::set_last_error("rt_render_dist: W and H must be > 0"); return RT_ERR_INVALID_ARG; }
-    const bool root = D.rank == 0;
-    if (root && !out_root) { rtamd::set_last_error("rt_render_dist: the root needs an output buffer"); return RT_ERR_INVALID_ARG; }
     std::lock_guard<std::mutex> lk(D.mu);
-    int rc = dist_init_streams(D);
-    if (rc != RT_OK) return rc;
-    const int S = strip_height(mode);
-    const std::vector<int32_t> rows = strip_rows(H, D.world, D.rank, S);
-    const int n = (int)rows.size();
-    const int m = max_rows(H, D.world, S);
-    const size_t row_elems = (size_t)W * 3;
-    const size_t row_bytes = row_elems * (kind ? 1 : sizeof(double));
+    if (D.dead) {
+        rtamd::set_last_error("rt_render_dist: this rank's communicator was aborted (" + D.dead_why +
+                              "); destroy the handle and create a new one");
+        return RT_ERR_HIP;
+    }
+    const bool root = D.rank == 0;
     const bool coll = D.collective();
+    const int inject = D.inject;
+    D.inject = 0;
+    // Local argument checks.  Without a collective they return at once; in a
+    // collective frame a failing rank still joins the frame's agreement (below)
+    // so that no peer waits for it.
+    int rc = RT_OK;
+    if (!s) { rtamd::set_last_error("rt_render_dist: scene is NULL"); rc = RT_ERR_INVALID_ARG; }
+    else if (W <= 0 || H <= 0) { rtamd::set_last_error("rt_render_dist: W and H must be > 0"); rc = RT_ERR_INVALID_ARG; }
+    else if (mode != RT_MODE_STANDARD && mode != RT_MODE_PAPER) { rtamd::set_last_error("rt_render_dist: bad mode"); rc = RT_ERR_INVALID_ARG; }
+    else if (root && !out_root) { rtamd::set_last_error("rt_render_dist: the root needs an output buffer"); rc = RT_ERR_INVALID_ARG; }
+    if (rc != RT_OK && !coll) return rc;
+    {
+        const int rs = dist_init_streams(D);   // the collective stream itself: without it nothing can be joined
+        if (rs != RT_OK) return rs;
+    }
+    if (coll) {
+        const int rx = dist_init_xchg(D);
+        if (rx != RT_OK) return rx;
+    }
+    const int Wc = std::max(W, 1), Hc = std::max(H, 1);
+    const int S = strip_height(mode == RT_MODE_PAPER ? RT_MODE_PAPER : RT_MODE_STANDARD);
+    const std::vector<int32_t> rows = strip_rows(Hc, D.world, D.rank, S);
+    const int n = (int)rows.size();
+    const int m = max_rows(Hc, D.world, S);
+    const size_t row_elems = (size_t)Wc * 3;
+    // paper mode (FP64) across ranks: each rank produces one paper-code byte
+    // per pixel, 1 B/px crosses xGMI, and the root decodes (k_place_codes)
+    const bool codes = coll && mode == RT_MODE_PAPER && !(flags & RT_FLAG_FP32);
+    const size_t row_bytes = codes ? (size_t)Wc : row_elems * (kind ? 1 : sizeof(double));   // gathered per row
     const auto bounds = chunk_bounds(m, coll ? kChunks : 1, S);
     const bool direct = !coll && kind == 0;   // trace straight into the caller's frame
-    if (!direct) HIP_TRY(D.mine.ensure(std::max<size_t>(1, (size_t)m * row_elems * sizeof(double))));
-    if (kind == 1 && coll) HIP_TRY(D.mine8.ensure(std::max<size_t>(1, (size_t)m * row_elems)));
     DevBuf& stage = D.sim_stage ? *D.sim_stage : D.stage;
-    if (coll && (root || D.sim_stage)) HIP_TRY(stage.ensure((size_t)D.world * m * row_bytes));
-    if (coll && root) {
+    auto fail = [&](int code, const char* what) {
+        if (rc == RT_OK) {
+            rc = code;
+            if (what) rtamd::set_last_error(std::string("rt_render_dist: ") + what);
+        }
+    };
+    // setup: buffers, the root's placement table, the frame
+    if (rc == RT_OK && !direct &&
+        D.mine.ensure(std::max<size_t>(1, (size_t)m * (codes ? (size_t)Wc : row_elems * sizeof(double)))) != hipSuccess)
+        fail(RT_ERR_HIP, "row buffer allocation failed");
+    if (rc == RT_OK && kind == 1 && coll && !codes && D.mine8.ensure(std::max<size_t>(1, (size_t)m * row_elems)) != hipSuccess)
+        fail(RT_ERR_HIP, "RGB8 row buffer allocation failed");
+    if (rc == RT_OK && coll && (root || D.sim_stage) && stage.ensure((size_t)D.world * m * row_bytes) != hipSuccess)
+        fail(RT_ERR_HIP, "gather stage allocation failed");
+    if (rc == RT_OK && coll && root) {
         // placement table: chunk k occupies slots [world*a, world*b) as [rank][b-a]
         D.rowtab_host.assign((size_t)D.world * m, -1);
         for (int r = 0; r < D.world; ++r) {
@@ -231,73 +411,173 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
                     D.rowtab_host[(size_t)D.world * ab.first + (size_t)r * (ab.second - ab.first) + (i - ab.first)] =
                         i < (int)rr.size() ? rr[i] : -1;
         }
-        HIP_TRY(D.rowtab.ensure(D.rowtab_host.size() * sizeof(int32_t)));
-        HIP_TRY(hipMemcpyAsync(D.rowtab.p, D.rowtab_host.data(), D.rowtab_host.size() * sizeof(int32_t),
-                               hipMemcpyHostToDevice, D.comm_st));
+        if (D.rowtab.ensure(D.rowtab_host.size() * sizeof(int32_t)) != hipSuccess ||
+            hipMemcpyAsync(D.rowtab.p, D.rowtab_host.data(), D.rowtab_host.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, D.comm_st) != hipSuccess)
+            fail(RT_ERR_HIP, "placement table upload failed");
     }
     rt_frame* f = nullptr;
-    rc = rt_frame_begin(s, W, H, mode, flags, rows.data(), n, st, &f);
-    if (rc != RT_OK) return rc;
+    if (rc == RT_OK) {
+        const int rb = rt_frame_begin(s, W, H, mode, flags, rows.data(), n, st, &f);
+        if (rb != RT_OK) rc = rb;   // (rt_frame_begin set the message)
+    }
+    if (!coll && rc != RT_OK) return rc;
+
+    // agreement 1 (collective frames): descriptor + setup status of every rank
+    int64_t* xd = D.xchg.as<int64_t>();
+    int64_t* xh = D.xchg_host;
+    const size_t n_desc = 2 * kDescFields + (size_t)D.world;
+    bool agreed = !coll;
+    if (coll) {
+        const int64_t v[kDescFields] = {W, H, mode, kind, flags};
+        for (int i = 0; i < kDescFields; ++i) {
+            xh[i] = v[i];
+            xh[kDescFields + i] = -v[i];
+        }
+        for (int r = 0; r < D.world; ++r) xh[2 * kDescFields + r] = (r == D.rank && rc != RT_OK) ? 1 : 0;
+        bool ok = hipMemcpyAsync(xd, xh, n_desc * sizeof(int64_t), hipMemcpyHostToDevice, D.comm_st) == hipSuccess;
+        if (ok && !D.sim_stage) ok = ncclAllReduce(xd, xd, n_desc, ncclInt64, ncclMax, D.comm, D.comm_st) == ncclSuccess;
+        if (ok) ok = hipMemcpyAsync(xh, xd, n_desc * sizeof(int64_t), hipMemcpyDeviceToHost, D.comm_st) == hipSuccess;
+        if (ok && inject == kInjectStall) {
+            int rate_khz = 100000;
+            (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, D.device);
+            const double stall_ms = std::min(D.timeout_ms * 4 + 1000, 10000.0);   // bounded: the wave always leaves
+            const unsigned long long ticks = (unsigned long long)rate_khz * (unsigned long long)stall_ms;
+            hipLaunchKernelGGL(k_test_stall, dim3(1), dim3(64), 0, D.comm_st, ticks);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        if (ok) ok = hipEventRecord(D.ev_desc, D.comm_st) == hipSuccess;
+        if (!ok) {
+            // this rank cannot take part in the frame's collectives: its peers
+            // will time out; abort so that nothing is left queued on them here
+            if (f) (void)rt_frame_end(f, nullptr);
+            dist_abort(D, "frame agreement could not be issued");
+            rtamd::set_last_error("rt_render_dist: the frame agreement could not be issued; communicator aborted");
+            return RT_ERR_HIP;
+        }
+    }
     double* fb_rows = direct ? static_cast<double*>(out_root) : D.mine.as<double>();
     int n_tb = 0, n_g = 0;
-    for (size_t k = 0; k < bounds.size() && rc == RT_OK; ++k) {
+    bool status_sent = false;
+    const size_t n_stat = (size_t)D.world;
+    for (size_t k = 0; k < bounds.size(); ++k) {
         const int a = bounds[k].first, b = bounds[k].second, hi = std::min(b, n);
         const hipStream_t cst = (k & 1) ? D.alt_st : st;   // chunks alternate between two streams
-        if (hi > a) rc = rt_frame_trace(f, a, hi, fb_rows + (size_t)a * row_elems, cst);
-        if (rc != RT_OK) break;
-        if (kind == 1 && hi > a) {
-            uint8_t* dst8 = coll ? D.mine8.as<uint8_t>() + (size_t)a * row_elems : static_cast<uint8_t*>(out_root);
-            if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) { rc = RT_ERR_HIP; break; }
-            rc = rt_framebuffer_to_rgb8_device(fb_rows + (size_t)a * row_elems, (size_t)(hi - a) * W, dst8, cst);
-            if (rc != RT_OK) break;
-            if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) { rc = RT_ERR_HIP; break; }
-        }
-        if (!coll) continue;
-        // chunk k -> root: ONE collective, ordered after the chunk's trace
-        if (hipEventRecord(D.ev_chunk[k], cst) != hipSuccess || hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess) {
-            rtamd::set_last_error("rt_render_dist: event chaining failed");
+        if (rc == RT_OK && inject == kInjectTraceFail && k == bounds.size() / 2) {
+            rtamd::set_last_error("rt_render_dist: injected trace failure (rt_test_dist_inject)");
             rc = RT_ERR_HIP;
-            break;
         }
-        if (hipEventRecord(D.ev_gs[n_g], D.comm_st) != hipSuccess) { rc = RT_ERR_HIP; break; }
-        const char* send = (kind ? D.mine8.as<char>() : D.mine.as<char>()) + (size_t)a * row_bytes;
+        if (rc == RT_OK && hi > a)
+            rc = codes ? rtamd::frame_trace_paper_codes(f, a, hi, D.mine.as<uint8_t>() + (size_t)a * row_bytes, cst)
+                       : rt_frame_trace(f, a, hi, fb_rows + (size_t)a * row_elems, cst);
+        if (rc == RT_OK && kind == 1 && hi > a && !codes) {
+            uint8_t* dst8 = coll ? D.mine8.as<uint8_t>() + (size_t)a * row_elems : static_cast<uint8_t*>(out_root);
+            if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) fail(RT_ERR_HIP, "event record failed");
+            if (rc == RT_OK) rc = rt_framebuffer_to_rgb8_device(fb_rows + (size_t)a * row_elems, (size_t)(hi - a) * W, dst8, cst);
+            if (rc == RT_OK && hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) fail(RT_ERR_HIP, "event record failed");
+        }
+        if (!coll) {
+            if (rc != RT_OK) break;
+            continue;
+        }
+        if (!agreed) {
+            // the descriptor reduction ran while chunk 0 was being traced
+            const int rw = dist_wait(D, D.ev_desc, "the frame agreement");
+            if (rw != RT_OK) {
+                if (f) (void)rt_frame_end(f, nullptr);
+                return rw;
+            }
+            std::string bad;
+            for (int i = 0; i < kDescFields; ++i) {
+                static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags"};
+                if (xh[i] != -xh[kDescFields + i]) bad += std::string(bad.empty() ? "" : ", ") + names[i];
+            }
+            std::string failed;
+            for (int r = 0; r < D.world; ++r)
+                if (xh[2 * kDescFields + r]) failed += (failed.empty() ? "" : ",") + std::to_string(r);
+            if (!bad.empty() || !failed.empty()) {
+                // every rank reaches this same verdict: no gather is issued anywhere
+                const int rl = rc;
+                const int re = f ? rt_frame_end(f, nullptr) : RT_OK;
+                (void)re;
+                if (rl != RT_OK) return rl;   // this rank's own failure (message already set)
+                if (!bad.empty()) {
+                    rtamd::set_last_error("rt_render_dist: the ranks disagree on the frame (" + bad + ")");
+                    return RT_ERR_INVALID_ARG;
+                }
+                rtamd::set_last_error("rt_render_dist: rank(s) " + failed + " failed to set up the frame");
+                return RT_ERR_HIP;
+            }
+            agreed = true;
+        }
+        // agreement 2: this rank's trace status, issued before the last
+        // gather (known here: the last chunk's trace is enqueued or skipped)
+        if (k + 1 == bounds.size()) {
+            int64_t* sd = xd + n_desc;
+            int64_t* sh = xh + n_desc;
+            for (int r = 0; r < D.world; ++r) sh[r] = (r == D.rank && rc != RT_OK) ? 1 : 0;
+            bool ok = hipMemcpyAsync(sd, sh, n_stat * sizeof(int64_t), hipMemcpyHostToDevice, D.comm_st) == hipSuccess;
+            if (ok && !D.sim_stage) ok = ncclAllReduce(sd, sd, n_stat, ncclInt64, ncclMax, D.comm, D.comm_st) == ncclSuccess;
+            if (ok) ok = hipMemcpyAsync(sh, sd, n_stat * sizeof(int64_t), hipMemcpyDeviceToHost, D.comm_st) == hipSuccess;
+            if (!ok) fail(RT_ERR_HIP, "trace status reduction could not be issued");
+            status_sent = ok;
+        }
+        // chunk k -> root: ONE collective, ordered after the chunk's trace
+        // (issued whatever happened locally: the peers are waiting for it)
+        if (rc == RT_OK && (hipEventRecord(D.ev_chunk[k], cst) != hipSuccess ||
+                            hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess))
+            fail(RT_ERR_HIP, "event chaining failed");
+        const bool timed = hipEventRecord(D.ev_gs[n_g], D.comm_st) == hipSuccess;
+        const char* send = (kind && !codes ? D.mine8.as<char>() : D.mine.as<char>()) + (size_t)a * row_bytes;
         const size_t chunk_bytes = (size_t)(b - a) * row_bytes;
         char* recv = stage.as<char>() + (size_t)D.world * a * row_bytes;
         if (D.sim_stage) {
             if (hipMemcpyAsync(recv + (size_t)D.rank * chunk_bytes, send, chunk_bytes, hipMemcpyDeviceToDevice,
-                               D.comm_st) != hipSuccess) {
-                rtamd::set_last_error("rt_test_render_dist_sim: copy failed");
-                rc = RT_ERR_HIP;
-                break;
-            }
+                               D.comm_st) != hipSuccess)
+                fail(RT_ERR_HIP, "simulated gather copy failed");
         } else {
-            const ncclResult_t r = ncclGather(send, root ? recv : nullptr, kind ? chunk_bytes : chunk_bytes / 8,
-                                              kind ? ncclUint8 : ncclFloat64, 0, D.comm, D.comm_st);
+            const bool bytes = kind || codes;
+            const ncclResult_t r = ncclGather(send, root ? recv : nullptr, bytes ? chunk_bytes : chunk_bytes / 8,
+                                              bytes ? ncclUint8 : ncclFloat64, 0, D.comm, D.comm_st);
             if (r != ncclSuccess) {
-                rtamd::set_last_error(std::string("ncclGather failed: ") + ncclGetErrorString(r));
-                rc = RT_ERR_HIP;
-                break;
+                fail(RT_ERR_HIP, nullptr);
+                rtamd::set_last_error(std::string("rt_render_dist: ncclGather failed: ") + ncclGetErrorString(r));
             }
         }
-        if (root && place_rows(recv, D.rowtab.as<int32_t>() + (size_t)D.world * a, D.world * (b - a), row_bytes,
-                               out_root, D.comm_st) != hipSuccess) {
-            rtamd::set_last_error("rt_render_dist: row placement failed");
-            rc = RT_ERR_HIP;
-            break;
+        if (root) {
+            const int32_t* slots = D.rowtab.as<int32_t>() + (size_t)D.world * a;
+            const hipError_t pe = codes ? place_codes(reinterpret_cast<const uint8_t*>(recv), slots, D.world * (b - a),
+                                                      Wc, kind, out_root, D.comm_st)
+                                        : place_rows(recv, slots, D.world * (b - a), row_bytes, out_root, D.comm_st);
+            if (pe != hipSuccess) fail(RT_ERR_HIP, "row placement failed");
         }
-        if (hipEventRecord(D.ev_ge[n_g++], D.comm_st) != hipSuccess) { rc = RT_ERR_HIP; break; }
+        if (timed && hipEventRecord(D.ev_ge[n_g], D.comm_st) == hipSuccess) ++n_g;
     }
     // alt_st's last work (a chunk's toByte) into st, which rt_frame_end synchronises
-    if (hipEventRecord(D.ev_alt, D.alt_st) != hipSuccess || hipStreamWaitEvent(st, D.ev_alt, 0) != hipSuccess) {
-        if (rc == RT_OK) rc = RT_ERR_HIP;
-    }
-    const int rc_end = rt_frame_end(f, stats);   // joins and synchronises the trace streams
-    if (coll && hipStreamSynchronize(D.comm_st) != hipSuccess && rc == RT_OK) {
-        rtamd::set_last_error("rt_render_dist: gather stream failed");
-        rc = RT_ERR_HIP;
+    if (hipEventRecord(D.ev_alt, D.alt_st) != hipSuccess || hipStreamWaitEvent(st, D.ev_alt, 0) != hipSuccess)
+        fail(RT_ERR_HIP, "stream join failed");
+    const int rc_end = f ? rt_frame_end(f, stats) : RT_OK;   // joins and synchronises the trace streams
+    if (coll) {
+        if (hipEventRecord(D.ev_desc, D.comm_st) != hipSuccess) {
+            dist_abort(D, "could not record the end of the frame's collectives");
+            rtamd::set_last_error("rt_render_dist: could not record the end of the frame's collectives; communicator aborted");
+            return RT_ERR_HIP;
+        }
+        const int rw = dist_wait(D, D.ev_desc, "the frame's gathers");
+        if (rw != RT_OK) return rw;
     }
     if (rc != RT_OK) return rc;
     if (rc_end != RT_OK) return rc_end;
+    if (coll && status_sent) {
+        std::string failed;
+        for (int r = 0; r < D.world; ++r)
+            if (xh[n_desc + r]) failed += (failed.empty() ? "" : ",") + std::to_string(r);
+        if (!failed.empty()) {
+            rtamd::set_last_error("rt_render_dist: rank(s) " + failed + " failed while tracing the frame" +
+                                  (root ? " (the gathered frame is incomplete)" : ""));
+            return RT_ERR_HIP;
+        }
+    }
     if (stats) {
         float ms = 0.f;
         // the collectives and placements themselves (each waits for its
@@ -331,6 +611,9 @@ void release_rank(rt_dist& d) {
     d.stage.release();
     d.rowtab.release();
     d.red.release();
+    d.xchg.release();
+    if (d.xchg_host) (void)hipHostFree(d.xchg_host);
+    d.xchg_host = nullptr;
     if (d.comm_st) (void)hipStreamDestroy(d.comm_st);
     if (d.alt_st) (void)hipStreamDestroy(d.alt_st);
     d.comm_st = d.alt_st = nullptr;
@@ -343,6 +626,7 @@ void release_rank(rt_dist& d) {
     for (auto& e : d.ev_gs) drop(e);
     for (auto& e : d.ev_ge) drop(e);
     drop(d.ev_alt);
+    drop(d.ev_desc);
     (void)hipSetDevice(prev);
 }
 
@@ -357,6 +641,7 @@ struct LocalGroup {
 
 std::mutex g_groups_mu;
 std::map<int, std::unique_ptr<LocalGroup>> g_groups;
+std::vector<std::unique_ptr<LocalGroup>> g_dropped;   // emptied groups whose lock may still be held
 
 // rt_shutdown: destroy every cached group (RCCL communicators, streams,
 // buffers).  Groups are created again on the next multi-GPU call.
@@ -376,7 +661,23 @@ int shutdown_groups() {
         ++n;
     }
     g_groups.clear();
+    g_dropped.clear();
     return n;
+}
+
+// Called with G->mu held by the caller (render_multi); takes the registry lock.
+void drop_group(int n, LocalGroup* G) {
+    for (auto& r : G->ranks) release_rank(*r);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(0);
+    G->out.release();
+    G->out8.release();
+    (void)hipSetDevice(prev);
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    auto it = g_groups.find(n);
+    if (it != g_groups.end() && it->second.get() == G) g_dropped.push_back(std::move(it->second));   // freed at rt_shutdown
+    if (it != g_groups.end()) g_groups.erase(it);
 }
 
 int local_group(int n, LocalGroup** out) {
@@ -399,6 +700,7 @@ int local_group(int n, LocalGroup** out) {
         D->world = n;
         D->rank = i;
         D->device = i;
+        D->timeout_ms = env_timeout_ms();
         D->comm = comms[i];
         D->own_comm = n > 1;
         G->ranks.push_back(std::move(D));
@@ -461,6 +763,11 @@ int render_multi(const rt_scene* s, int W, int H, int mode, int flags, int n_gpu
     (void)hipSetDevice(0);
     for (int i = 0; i < n; ++i)
         if (rcs[i] != RT_OK) {
+            // a rank whose communicator was aborted leaves the group unusable:
+            // drop it (the next call creates the communicators again)
+            bool dead = false;
+            for (auto& r : G->ranks) dead = dead || r->dead;
+            if (dead) drop_group(n, G);
             rtamd::set_last_error("device " + std::to_string(i) + ": " + errs[i]);
             (void)hipSetDevice(prev_dev);
             return rcs[i];
@@ -539,6 +846,7 @@ extern "C" int rt_dist_create(const uint8_t id[RT_DIST_ID_BYTES], int world, int
     std::unique_ptr<rt_dist> D(new rt_dist);
     D->world = world;
     D->rank = rank;
+    D->timeout_ms = env_timeout_ms();
     HIP_TRY(hipGetDevice(&D->device));
     if (world > 1) {
         ncclUniqueId u;
@@ -547,6 +855,13 @@ extern "C" int rt_dist_create(const uint8_t id[RT_DIST_ID_BYTES], int world, int
         D->own_comm = true;
     }
     *out = D.release();
+    return RT_OK;
+}
+
+extern "C" int rt_dist_set_timeout(rt_dist* d, int timeout_ms) {
+    if (!d || timeout_ms <= 0) { rtamd::set_last_error("rt_dist_set_timeout: bad arguments"); return RT_ERR_INVALID_ARG; }
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->timeout_ms = timeout_ms;
     return RT_OK;
 }
 
@@ -598,6 +913,35 @@ extern "C" int rt_test_render_dist_sim(const rt_scene* s, int W, int H, int mode
     stage.release();
     out.release();
     return rc;
+}
+
+// ------------------------------------------------------------- test hook
+// One simulated rank of a world-`world` frame on the current device, through
+// the product's rank path (dist_frame: partition, chunks on two streams,
+// paper codes, the gather stage and, on rank 0, the placement), the RCCL
+// gather replaced by a device copy into a shared stage.  Ranks are cached per
+// (world, rank), so repeated calls time a warm rank (tools/sim_ranks.py).
+extern "C" int rt_test_dist_sim_rank(const rt_scene* s, int W, int H, int mode, int flags, int world, int rank,
+                                     int rgb8, rt_stats* stats) {
+    if (!s || W <= 0 || H <= 0 || world <= 0 || rank < 0 || rank >= world) return RT_ERR_INVALID_ARG;
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::unique_ptr<rt_dist>> ranks;
+    static DevBuf stage, out;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& d = ranks[{world, rank}];
+    if (!d) {
+        d.reset(new rt_dist);
+        d->world = world;
+        d->rank = rank;
+        d->sim_stage = &stage;
+        HIP_TRY(hipGetDevice(&d->device));
+    }
+    void* o = nullptr;
+    if (rank == 0) {
+        HIP_TRY(out.ensure((size_t)W * H * 3 * (rgb8 ? 1 : sizeof(double))));
+        o = out.p;
+    }
+    return dist_frame(*d, s, W, H, mode, flags, rgb8 ? 1 : 0, o, nullptr, stats);
 }
 
 // ---------------------------------------- launcher plumbing over RCCL
@@ -667,11 +1011,24 @@ extern "C" int rt_test_dist_create_rccl1(rt_dist** out) {
     D->world = 1;
     D->rank = 0;
     D->force_collective = true;
+    D->timeout_ms = env_timeout_ms();
     HIP_TRY(hipGetDevice(&D->device));
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     NCCL_TRY(ncclCommInitRank(&D->comm, 1, u, 0));
     D->own_comm = true;
     *out = D.release();
+    return RT_OK;
+}
+
+// ------------------------------------------------------------- test hook
+// Fault injection on the next frame of d: 1 = this rank's trace fails at its
+// middle chunk (a rank-local failure after the frame agreement), 2 = the
+// collective stream is held past the rank's timeout (a peer that never
+// arrives: the wait times out and the communicator is aborted).
+extern "C" int rt_test_dist_inject(rt_dist* d, int what) {
+    if (!d || what < 0 || what > 2) return RT_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->inject = what;
     return RT_OK;
 }

@@ -264,6 +264,7 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     const int cm = P.mat[ci];
     // get_edge_strength (tracer.cpp:133-178): neighbours (-1,0) (1,0) (0,-1) (0,1)
     real maxEdge = RV(0.0);
+    int eidx = 0;   // index of maxEdge in {0, 0.3, 0.5, 0.6, 0.9} (rtamd::paper_code)
     int valid = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -277,19 +278,36 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
         const bool nh = P.hit[ni] != 0;
         if (ch != nh) {
             maxEdge = dmax(maxEdge, RV(0.9));
+            eidx = max(eidx, 4);
             continue;
         }
         if (ch && nh) {
             const real nt = P.t[ni];
             const real minD = dmin(ct, nt), maxD = dmax(ct, nt);
-            if (minD > RV(1e-4) && maxD / minD > RV(3.0)) maxEdge = dmax(maxEdge, RV(0.6));
+            if (minD > RV(1e-4) && maxD / minD > RV(3.0)) {
+                maxEdge = dmax(maxEdge, RV(0.6));
+                eidx = max(eidx, 3);
+            }
             const real nd = dot3(cn, v3(P.nx[ni], P.ny[ni], P.nz[ni]));
-            if (nd < RV(0.2)) maxEdge = dmax(maxEdge, RV(0.5));
-            if (cm != P.mat[ni] && nd < RV(0.7)) maxEdge = dmax(maxEdge, RV(0.3));
+            if (nd < RV(0.2)) {
+                maxEdge = dmax(maxEdge, RV(0.5));
+                eidx = max(eidx, 2);
+            }
+            if (cm != P.mat[ni] && nd < RV(0.7)) {
+                maxEdge = dmax(maxEdge, RV(0.3));
+                eidx = max(eidx, 1);
+            }
         }
     }
     if (valid < 4) maxEdge *= RV(0.5);
     const real edge = maxEdge;
+    if (P.code) {
+        // distributed frames: the pixel's place in the output alphabet
+        // (rtamd::paper_code), decoded bit-exactly on the root after the gather
+        const bool h = edge <= RV(0.5) && crosshatch(P.lum[ci], x, y) != RV(0.0);
+        P.code[(size_t)ri * P.W + x] = (uint8_t)(eidx | (valid < 4 ? 8 : 0) | (h ? 16 : 0));
+        return;
+    }
     V3 o;
     if (edge > RV(0.8)) {
         o = v3(RV(0.0), RV(0.0), RV(0.0));

@@ -113,8 +113,32 @@ struct PaperParams {
     double* nz;
     double* lum;
     double* fb;
+    uint8_t* code;               // non-null: k_paper_finish writes paper_code bytes [n_rows*W] instead of fb
     unsigned long long* counters;
 };
+
+// Paper mode's output alphabet (tracer.cpp:258-281): every pixel is grey
+// (r = g = b) and a function of the edge strength - the max of the constants
+// {0.9, 0.6, 0.5, 0.3} over the neighbour tests, or 0, halved when a
+// neighbour lies outside the frame (tracer.cpp:133-178) - and of the hatch
+// bit apply_crosshatch returns (tracer.cpp:188-205).  So one byte holds a
+// pixel exactly: bits 0-2 the index of the max in {0, 0.3, 0.5, 0.6, 0.9},
+// bit 3 the halving, bit 4 the hatch bit (white).  The distributed frame
+// gathers these bytes (1 B/px instead of 24) and the root decodes them with
+// the reference's own FP64 expression, bit for bit.
+__host__ __device__ inline double paper_code_value(unsigned code) {
+    const unsigned i = code & 7;
+    double edge = i == 1 ? 0.3 : i == 2 ? 0.5 : i == 3 ? 0.6 : i == 4 ? 0.9 : 0.0;
+    if (code & 8) edge *= 0.5;
+    if (edge > 0.8) return 0.0;
+    if (edge > 0.5) return 0.2;
+    double o = (code & 16) ? 1.0 : 0.0;
+    if (edge > 0.3) {
+        const double darken = (edge - 0.3) * 0.4;
+        o *= (1.0 - darken);
+    }
+    return o;
+}
 
 // Per-lane stacks of the render kernels (checked on the host per scene).
 // The common kernels carry small ones; scenes beyond them run on the

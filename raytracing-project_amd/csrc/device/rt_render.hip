@@ -190,7 +190,8 @@ struct rt_frame {
     // paper mode: ext = rendered rows and their vertical neighbours
     int n_ext = 0;
     std::vector<int32_t> ext_pos;              // output row -> ext index (-1: none)
-    std::vector<char> ext_done;                // primary hit already launched
+    std::vector<int> ext_done;                 // primary hit launched by trace call (value - 1); 0 = not yet
+    std::vector<hipStream_t> call_st;          // stream of each trace call
     int list_used = 0;                         // ext-list entries consumed in the aux buffer
     int n_tev = 0;                             // trace events recorded (ws.tev[0 .. n_tev))
     hipStream_t last_st = nullptr;             // stream of the previous trace call
@@ -512,22 +513,44 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     return RT_OK;
 }
 
-int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
+// fb: FP64 rows; codes (paper mode, FP64 kernels only): one paper_code byte
+// per pixel instead (rtamd::frame_trace_paper_codes).
+int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8_t* codes = nullptr) {
     if (!f) { rtamd::set_last_error("rt_frame_trace: frame is NULL"); return RT_ERR_INVALID_ARG; }
     if (ri0 < 0 || ri1 < ri0 || ri1 > f->n_rows) { rtamd::set_last_error("rt_frame_trace: bad row range"); return RT_ERR_INVALID_ARG; }
     if (ri1 == ri0) return RT_OK;
-    if (!fb) { rtamd::set_last_error("rt_frame_trace: fb is NULL"); return RT_ERR_INVALID_ARG; }
+    if (!fb && !codes) { rtamd::set_last_error("rt_frame_trace: fb is NULL"); return RT_ERR_INVALID_ARG; }
+    if (codes && (f->mode != RT_MODE_PAPER || f->fp32)) {
+        rtamd::set_last_error("rt_frame_trace: paper codes need a paper-mode FP64 frame");
+        return RT_ERR_INVALID_ARG;
+    }
     Workspace& ws = *f->ws;
     const hipStream_t st = hs ? hs : f->st;
     const int W = f->W, n = ri1 - ri0;
     unsigned long long* ctr = ws.counters.as<unsigned long long>();
     // another stream first waits for the scene upload and jitter (begin); in
-    // paper mode a chunk also reads primary hits an earlier chunk computed,
-    // so chunks on different streams are chained
+    // paper mode a chunk that reads primary hits an earlier call computed on
+    // another stream waits for that call (adjacent strips share a neighbour
+    // row: one rank's whole frame; a rank of a split frame traces strips that
+    // share none, so its chunks overlap on the two streams)
     const auto t_launch = SClock::now();
     if (st != f->st) HIP_TRY(hipStreamWaitEvent(st, ws.ev[1], 0));
-    if (f->mode == RT_MODE_PAPER && f->n_tev > 0 && f->last_st != st)
-        HIP_TRY(hipStreamWaitEvent(st, ws.tev[f->n_tev - 1], 0));
+    if (f->mode == RT_MODE_PAPER && f->n_tev > 0) {
+        std::vector<char> wait(f->n_tev, 0);
+        for (int i = ri0; i < ri1; ++i) {
+            const int r = f->rows[i];
+            for (int rr = r - 1; rr <= r + 1; ++rr) {
+                if (rr < 0 || rr >= f->H) continue;
+                const int e = f->ext_pos[rr];
+                if (e >= 0 && f->ext_done[e]) {
+                    const int c = f->ext_done[e] - 1;   // the call that computed it
+                    if (f->call_st[c] != st) wait[c] = 1;
+                }
+            }
+        }
+        for (int c = 0; c < f->n_tev; ++c)
+            if (wait[c]) HIP_TRY(hipStreamWaitEvent(st, ws.tev[c], 0));
+    }
     if (f->mode == RT_MODE_STANDARD) {
         StdParams P;
         P.W = W;
@@ -556,7 +579,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
                 if (rr < 0 || rr >= f->H) continue;
                 const int e = f->ext_pos[rr];
                 if (e >= 0 && !f->ext_done[e]) {
-                    f->ext_done[e] = 1;
+                    f->ext_done[e] = f->n_tev + 1;   // (this call's index + 1)
                     if (rr != prev_row + 1)
                         while (list.size() % 8) list.push_back(-1);
                     list.push_back(e);
@@ -588,6 +611,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         P.nz = dd + 3 * npx;
         P.lum = dd + 4 * npx;
         P.fb = fb;
+        P.code = codes;
         P.counters = ctr;
         if (!list.empty()) {
             if ((size_t)f->list_used + list.size() > 8 * (size_t)n_ext) {
@@ -620,6 +644,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs) {
         ws.tev.push_back(e);
     }
     HIP_TRY(hipEventRecord(ws.tev[f->n_tev], st));
+    f->call_st.push_back(st);
     ++f->n_tev;
     f->last_st = st;
     f->traced = true;
@@ -778,6 +803,18 @@ extern "C" int rt_stream_destroy(void* stream) {
     return RT_OK;
 }
 
+extern "C" int rt_host_register(void* host, size_t bytes) {
+    if (!host || !bytes) { rtamd::set_last_error("rt_host_register: NULL or empty"); return RT_ERR_INVALID_ARG; }
+    HIP_TRY(hipHostRegister(host, bytes, hipHostRegisterDefault));
+    return RT_OK;
+}
+
+extern "C" int rt_host_unregister(void* host) {
+    if (!host) { rtamd::set_last_error("rt_host_unregister: NULL"); return RT_ERR_INVALID_ARG; }
+    HIP_TRY(hipHostUnregister(host));
+    return RT_OK;
+}
+
 extern "C" int rt_render_rows_device(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host,
                                      int n_rows, double* fb_rows_dev, void* hip_stream, rt_stats* stats) {
     return render_rows_impl(s, W, H, mode, flags, rows_host, n_rows, fb_rows_dev, (hipStream_t)hip_stream, stats);
@@ -793,6 +830,10 @@ extern "C" int rt_frame_trace(rt_frame* f, int ri0, int ri1, double* fb_rows_dev
 }
 
 extern "C" int rt_frame_end(rt_frame* f, rt_stats* stats) { return frame_end(f, stats); }
+
+int rtamd::frame_trace_paper_codes(rt_frame* f, int ri0, int ri1, uint8_t* codes_rows_dev, void* hip_stream) {
+    return frame_trace(f, ri0, ri1, nullptr, (hipStream_t)hip_stream, codes_rows_dev);
+}
 
 extern "C" int rt_render(const rt_scene* s, int W, int H, int mode, int flags, double* fb_host, rt_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();

@@ -16,4 +16,8 @@ bool node_depth_ok(const rt_scene_desc& d, int idx, int level, int* maxdepth);
 uint64_t scene_uid(const rt_scene* s);
 // librtamd: free every per-device workspace (rt_shutdown); returns an rt_status.
 int release_device_workspaces();
+// librtamd: rt_frame_trace of a paper-mode FP64 frame that writes one
+// paper-code byte per pixel (rtamd::paper_code_value) instead of FP64 rows:
+// the distributed frame's gather payload (rt_dist.hip).
+int frame_trace_paper_codes(rt_frame* f, int ri0, int ri1, uint8_t* codes_rows_dev, void* hip_stream);
 }  // namespace rtamd

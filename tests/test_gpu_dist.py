@@ -210,6 +210,81 @@ def test_rccl_world1_collective_path(gpu, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg4_std", "cfg5_paper"])
+def test_rccl_world1_injected_trace_failure_then_recovers(gpu, name):
+    """A rank-local failure in the middle of a collective frame (the trace of
+    the middle chunk fails after the frame agreement): the rank still issues
+    every gather and the trace-status reduction, the call returns RT_ERR_HIP
+    naming the failed rank, and the next frame on the same communicator
+    renders bit-equal to rt_render (HIP/RCCL errors checked and
+    returned; nothing left blocked)."""
+    sc, mode = _scene(gpu, name)
+    W, H = sc.width, sc.height
+    lib = gpu.amd_lib()
+    lib.rt_test_dist_inject.argtypes = [C.c_void_p, C.c_int]
+    d = C.c_void_p()
+    assert lib.rt_test_dist_create_rccl1(C.byref(d)) == 0, gpu.last_error()
+    try:
+        want = gpu.Tracer(sc, W, H, mode).render()
+        out = gpu.DeviceBuffer(H * W * 3 * 8)
+        st = gpu.Stats()
+        assert lib.rt_test_dist_inject(d, 1) == 0
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, None, C.byref(st))
+        assert rc == -5 and "injected trace failure" in gpu.last_error()
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, None, C.byref(st))
+        assert rc == 0, gpu.last_error()
+        assert np.array_equal(out.to_host(np.float64, (H, W, 3)), want)
+        assert lib.rt_dist_barrier(d) == 0
+    finally:
+        lib.rt_dist_destroy(d)
+
+
+@pytest.mark.gpu
+def test_rccl_world1_peer_timeout_aborts(gpu):
+    """A peer that never arrives (the collective stream held past the rank's
+    timeout by a bounded kernel): the wait gives up after the timeout instead
+    of blocking, the communicator is aborted (ncclCommAbort), the handle then
+    refuses frames with a message, and a new handle renders normally."""
+    import time
+
+    sc, mode = _scene(gpu, "cfg4_std")
+    W, H = sc.width, sc.height
+    lib = gpu.amd_lib()
+    lib.rt_test_dist_inject.argtypes = [C.c_void_p, C.c_int]
+    lib.rt_dist_set_timeout.argtypes = [C.c_void_p, C.c_int]
+    out = gpu.DeviceBuffer(H * W * 3 * 8)
+    st = gpu.Stats()
+    d = C.c_void_p()
+    assert lib.rt_test_dist_create_rccl1(C.byref(d)) == 0, gpu.last_error()
+    try:
+        assert lib.rt_dist_set_timeout(d, 300) == 0
+        assert lib.rt_test_dist_inject(d, 2) == 0
+        stream = gpu.Stream()
+        t0 = time.monotonic()
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, stream.handle, C.byref(st))
+        took = time.monotonic() - t0
+        # the message proves the wait gave up at the timeout (had it waited for
+        # the 2.2 s holding kernel, the agreement would have completed)
+        assert rc == -5 and "timed out after 300 ms" in gpu.last_error(), gpu.last_error()
+        assert took < 3.5, took
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, stream.handle, C.byref(st))
+        msg = gpu.last_error()
+        print(f"timeout path: first call {took:.3f} s; then: {msg}")
+        assert rc == -5 and "aborted" in msg
+        stream.destroy()
+    finally:
+        lib.rt_dist_destroy(d)   # waits for the (bounded) holding kernel
+    d = C.c_void_p()
+    assert lib.rt_test_dist_create_rccl1(C.byref(d)) == 0, gpu.last_error()
+    try:
+        rc = lib.rt_render_dist(d, sc.handle, W, H, mode, 0, out.ptr, None, C.byref(st))
+        assert rc == 0, gpu.last_error()
+        assert np.array_equal(out.to_host(np.float64, (H, W, 3)), gpu.Tracer(sc, W, H, mode).render())
+    finally:
+        lib.rt_dist_destroy(d)
+
+
+@pytest.mark.gpu
 def test_render_multi_all_visible_devices(gpu):
     """rt_render_multi / rt_render_rgb8 over every visible device (RCCL
     ncclCommInitAll + ncclGather) equal rt_render bit for bit."""

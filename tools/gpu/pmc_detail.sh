@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 CFG=${1:-4}
-OUT=gpurun_out/pmc_detail
+OUT=gpurun_out/pmc_detail_$CFG
 rm -rf $OUT; mkdir -p $OUT
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32" \
@@ -13,9 +13,9 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_ADD_F64 SQ_
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o pmc -- python3 tools/one_frame.py --config $CFG --frames 2 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/pmc_summary.py $OUT > /dev/null && python3 - <<'PY'
+python3 tools/pmc_summary.py $OUT > /dev/null && python3 - $CFG <<'PY'
 import json
-d = json.load(open("gpurun_out/pmc_detail/summary.json"))
+d = json.load(open(f"gpurun_out/pmc_detail_{__import__('sys').argv[1]}/summary.json"))
 for k, m in d.items():
     if "k_std" not in k and "k_paper" not in k:
         continue

@@ -44,8 +44,13 @@ def main():
     ap.add_argument("--rgb8", action="store_true", help="gather 3 B/px (the CLI path) instead of FP64")
     ap.add_argument("--one-stream", dest="two_streams", action="store_false",
                     help="all chunks on one stream (the product alternates two, rt_dist.hip)")
+    ap.add_argument("--legacy", action="store_true",
+                    help="time rt_frame_* chunks directly (FP64 rows) instead of the product's rank path "
+                         "(rt_test_dist_sim_rank: paper codes, placement on rank 0)")
     ap.set_defaults(two_streams=True)
     args = ap.parse_args()
+    if not args.legacy:
+        return product_ranks(args)
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
@@ -124,6 +129,58 @@ def main():
                "speedup_before_gather": round(base / worst, 3) if base else None,
                "gather_bytes_per_rank": m * W * bpp, "exposed_gather_ms_64GBs": round(g64, 3),
                "exposed_gather_ms_153GBs": round(g153, 3),
+               "projected_speedup_64GBs": round(base / (worst + g64), 3) if base else None,
+               "projected_speedup_153GBs": round(base / (worst + g153), 3) if base else None}
+        print(json.dumps(out), flush=True)
+
+
+def product_ranks(args):
+    """Every rank's share through the product's rank path on this GPU
+    (rt_test_dist_sim_rank: rt_render_dist's dist_frame with the RCCL gather
+    replaced by a device copy; rank 0 also places/decodes every slot).  The
+    exposed gather is modelled as the last chunk's bytes over one xGMI link."""
+    text, mode = scenes.config_json(args.config)
+    sc = rtamd.load_scene_from_json_text(text)
+    W, H = sc.width, sc.height
+    lib = rtamd.amd_lib()
+    lib.rt_test_dist_sim_rank.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.POINTER(rtamd.Stats)]
+    st = rtamd.Stats()
+    rgb8 = 1 if args.rgb8 else 0
+    base = None
+    for N in [int(v) for v in args.worlds.split(",")]:
+        per = []
+        for r in range(N):
+            def run():
+                rc = lib.rt_test_dist_sim_rank(sc.handle, W, H, mode, 0, N, r, rgb8, C.byref(st))
+                assert rc == 0, rtamd.last_error()
+            run()
+            wall, ker = [], []
+            for _ in range(args.reps):
+                rtamd.device_synchronize()
+                t0 = time.perf_counter()
+                run()
+                wall.append((time.perf_counter() - t0) * 1e3)
+                ker.append(st.ms_kernel)
+            per.append({"rank": r, "wall_ms": min(wall), "kernel_ms": min(ker),
+                        "rays": st.rays_intersect + st.rays_occluded})
+        worst = max(p["wall_ms"] for p in per)
+        if base is None and N == 1:
+            base = worst
+        rows = rtamd.dist_rows(H, N, 0, mode)
+        strip = frame_dist.strip_for(mode)
+        a_last, b_last = frame_dist.chunk_bounds(len(rows), 4, strip)[-1]
+        bpp = 1 if mode == 1 else (3 if args.rgb8 else 24)   # paper: one code byte per pixel
+        last_chunk = (b_last - a_last) * W * bpp
+        g64 = last_chunk / 64e9 * 1e3 if N > 1 else 0.0
+        g153 = last_chunk / 153e9 * 1e3 if N > 1 else 0.0
+        out = {"config": args.config, "world": N, "path": "product rank (rt_test_dist_sim_rank)",
+               "max_rank_wall_ms": round(worst, 3), "rank0_wall_ms": round(per[0]["wall_ms"], 3),
+               "min_rank_wall_ms": round(min(p["wall_ms"] for p in per), 3),
+               "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
+               "gather_bytes_per_rank": len(rows) * W * bpp,
+               "speedup_before_gather": round(base / worst, 3) if base else None,
+               "exposed_gather_ms_64GBs": round(g64, 4), "exposed_gather_ms_153GBs": round(g153, 4),
                "projected_speedup_64GBs": round(base / (worst + g64), 3) if base else None,
                "projected_speedup_153GBs": round(base / (worst + g153), 3) if base else None}
         print(json.dumps(out), flush=True)
