@@ -228,8 +228,11 @@ enum rt_flags {
     RT_FLAG_FP32 = 4,           /* NON-PARITY fast path: trace in
                                    FP32 on float copies of the scene; framebuffer stays
                                    double.  Not within the 1e-5 parity tolerance.   */
-    RT_FLAG_NO_BVH = 8          /* scenes of more than 64 objects: wave-level culling
-                                   without the wave BVH (A/B; results are identical) */
+    RT_FLAG_NO_BVH = 8          /* scenes of more than 256 top-level objects (the wave
+                                   BVH threshold kWaveBvhMin, scene_compile.hpp) and no
+                                   eager programs: wave-level culling without the wave
+                                   BVH (A/B; results are identical).  No effect on
+                                   smaller scenes, which never build the BVH.        */
 };
 
 /* Tracer::render: render the whole frame into a caller-owned host buffer of
@@ -242,7 +245,8 @@ int rt_render(const rt_scene* s, int W, int H, int mode, int flags,
 
 /* Tracer::render over n_gpus HIP devices of THIS process (n_gpus <= 0: all
  * visible devices): every device renders interleaved strips of RT_STRIP_ROWS
- * (paper mode: RT_PAPER_STRIP_ROWS) output rows (strip s -> device s mod n, rt_dist_rows), and the strips reach
+ * (paper mode: RT_PAPER_STRIP_ROWS) output rows (a weighted round robin over the strips, rotated every
+ * round, device 0 lighter for its placement work: rt_dist_rows_mode), and the strips reach
  * device 0 through RCCL ncclGather over xGMI (one collective per row chunk,
  * overlapped with the tracing of the next chunk) before the one D2H copy into
  * fb_host.  The result is bit-identical to rt_render (same kernels, same
@@ -298,8 +302,9 @@ int rt_dist_barrier(rt_dist* d);
  * timeout is RT_DIST_TIMEOUT_MS from the environment at creation (default
  * 120000) or rt_dist_set_timeout. */
 int rt_dist_set_timeout(rt_dist* d, int timeout_ms);
-/* The partition: writes the output rows of `rank` (ascending) to rows_out
- * (room for H entries) and returns their count; <0 on bad arguments.
+/* The partition of an FP64 frame: writes the output rows of `rank`
+ * (ascending) to rows_out (room for H entries) and returns their count; <0
+ * on bad arguments.  (RGB8 frames weight every rank equally.)
  * rt_dist_rows is the standard-mode partition (RT_STRIP_ROWS); paper mode
  * uses RT_PAPER_STRIP_ROWS strips (rt_dist_rows_mode). */
 int rt_dist_rows(int H, int world, int rank, int32_t* rows_out);

@@ -300,6 +300,9 @@ struct DevScene {
     const DevOp* ops;
     const float* gb;    // OP_IVL_GROUP bounds (cx, cy, cz, r), f32-inflated
     const float4* ctab; // per object 2 x float4: wave-level cull record (CompiledScene::ctab)
+    const float4* lrec; // [light][object] 2 x float4: light-relative shadow cull records (CompiledScene::lrec / lwrec)
+    const float4* lgb;  // [light][gb ball] 2 x float4 (CompiledScene::lgb)
+    int n_gb;
     const FoldT* fold;  // fold objects' leaf tables (DevObj::fold0)
     int n_lights, n_objs;
     int n_dlights;
@@ -1470,17 +1473,6 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
 
 
 // ------------------------------------------- wave-level shadow-ray culling
-// A shadow query of a whole wave (every lane active; lanes that need no
-// query pass need = false) is culled object by object in ONE transposed
-// test instead of one wave-uniform ball test per object: the segments
-// [o + tmin d, o + tmax d] of all querying lanes lie inside the capsule of
-// radius rho around [C0, C1], C0 / C1 the first querying lane's endpoints
-// and rho the largest distance of any lane's endpoint from them (a point
-// (1-s) A_i + s B_i is within (1-s)|A_i - C0| + s|B_i - C1| of the axis).
-// Lane j then tests object j's bounding ball against that capsule, and one
-// ballot gives the objects any lane can reach.  Like ball_touch the test is
-// conservative in f32 (a margin of 1e-5 of every magnitude involved), so it
-// never drops an object some lane's segment touches: results are unchanged.
 // Every lane of the wave active AT THIS POINT.  The transposed tests (lane j
 // tests object / leaf j for the whole wave) and the DPP / readlane bundle
 // reductions are valid only then, so each of them checks the exec mask where
@@ -1516,14 +1508,6 @@ __device__ __forceinline__ float uni(float v) {
 }
 
 
-// A shadow bundle's capsule (wave-uniform): radius rho around the segment
-// [a, b], u = b - a, iuu = 1 / |u|^2 (0 for a point), m5 = 1e-5 * the
-// bundle's magnitude and rm5 = rho + m5 (the margins' uniform parts).
-struct Capsule {
-    f2v axy, bxy, uxy;
-    float az, bz, uz, iuu, rho, m5, rm5;
-    f2v abx, aby, abz;   // (a.x, b.x), ... for the half-space test
-};
 // A bundle's cone (or double cone, for lines): origins within rho of o,
 // directions within theta of a (cth = cos theta, sth = sin theta).
 struct Cone {
@@ -1533,23 +1517,6 @@ struct Cone {
 // |x| + |y| + |z| + r of a ball (the records carry it precomputed)
 __device__ __forceinline__ float ball_mag(const float4 g) {
     return __builtin_fabsf(g.x) + __builtin_fabsf(g.y) + __builtin_fabsf(g.z) + g.w;
-}
-
-__device__ __forceinline__ bool capsule_touch(const float4 g, float gmag, const Capsule& K) {
-    const f2v wxy = f2(g.x, g.y) - K.axy;
-    const float wz = g.z - K.az;
-    const float wu = dot_pk(wxy, wz, K.uxy, K.uz);
-    // (iuu = 0 for a point capsule: s = 0; a non-finite wu makes q NaN: passes)
-    const float s = __builtin_amdgcn_fmed3f(wu * K.iuu, 0.0f, 1.0f);
-    const f2v qxy = pk_fma(f2s(-s), K.uxy, wxy);
-    const float qz = __builtin_fmaf(-s, K.uz, wz);
-    const float d2 = dot_pk(qxy, qz, qxy, qz);
-    const float R = g.w + K.rho + __builtin_fmaf(1e-5f, gmag, K.m5);
-    return !(d2 > R * R);   // NaN passes
-}
-__device__ __forceinline__ bool capsule_touch(const float* g, const Capsule& K) {
-    const float4 b = *reinterpret_cast<const float4*>(g);
-    return capsule_touch(b, ball_mag(b), K);
 }
 
 // The same bundle seen as LINES (Primitive::interval has no range, so a CSG
@@ -1582,6 +1549,59 @@ template <class CT>
 __device__ __forceinline__ void cnt_add(CT& cnt, int k, int n) {
     for (int i = 0; i < n; ++i) cnt.inc(k);
 }
+// Objects a culled BVH chunk holds (op-counting builds: RT_OPC_CULLED counts
+// every object a query skipped, whether by its own test or its chunk's)
+__device__ __forceinline__ int chunk_objects(const DevScene& S, int base) {
+    int n = 0;
+    for (int o = base; o < S.n_objs && o < base + 64; ++o) {
+        const int k = S.objs[o].kind;
+        n += (k != rtamd::OBJ_GROUP && k != rtamd::OBJ_NEVER) ? 1 : 0;
+    }
+    return n;
+}
+
+
+// ------------------------------------------------- capsule shadow culls
+// A shadow query of a whole wave (every lane active; lanes that need no
+// query pass need = false) is culled object by object in ONE transposed
+// test instead of one wave-uniform ball test per object: the segments
+// [o + tmin d, o + tmax d] of all querying lanes lie inside the capsule of
+// radius rho around [C0, C1], C0 / C1 the first querying lane's endpoints
+// and rho the largest distance of any lane's endpoint from them (a point
+// (1-s) A_i + s B_i is within (1-s)|A_i - C0| + s|B_i - C1| of the axis).
+// Lane j then tests object j's bounding ball against that capsule, and one
+// ballot gives the objects any lane can reach.  Like ball_touch the test is
+// conservative in f32 (a margin of 1e-5 of every magnitude involved), so it
+// never drops an object some lane's segment touches: results are unchanged.
+// The kernels without the wave BVH use it (configs 1-6: at most a few dozen
+// objects, one transposed test per query); the BVH kernels use the
+// light-centred culls below.
+//
+// A shadow bundle's capsule (wave-uniform): radius rho around the segment
+// [a, b], u = b - a, iuu = 1 / |u|^2 (0 for a point), m5 = 1e-5 * the
+// bundle's magnitude and rm5 = rho + m5 (the margins' uniform parts).
+struct Capsule {
+    f2v axy, bxy, uxy;
+    float az, bz, uz, iuu, rho, m5, rm5;
+    f2v abx, aby, abz;   // (a.x, b.x), ... for the half-space test
+};
+__device__ __forceinline__ bool capsule_touch(const float4 g, float gmag, const Capsule& K) {
+    const f2v wxy = f2(g.x, g.y) - K.axy;
+    const float wz = g.z - K.az;
+    const float wu = dot_pk(wxy, wz, K.uxy, K.uz);
+    // (iuu = 0 for a point capsule: s = 0; a non-finite wu makes q NaN: passes)
+    const float s = __builtin_amdgcn_fmed3f(wu * K.iuu, 0.0f, 1.0f);
+    const f2v qxy = pk_fma(f2s(-s), K.uxy, wxy);
+    const float qz = __builtin_fmaf(-s, K.uz, wz);
+    const float d2 = dot_pk(qxy, qz, qxy, qz);
+    const float R = g.w + K.rho + __builtin_fmaf(1e-5f, gmag, K.m5);
+    return !(d2 > R * R);   // NaN passes
+}
+__device__ __forceinline__ bool capsule_touch(const float* g, const Capsule& K) {
+    const float4 b = *reinterpret_cast<const float4*>(g);
+    return capsule_touch(b, ball_mag(b), K);
+}
+
 
 // Lane j's transposed test of object j's cull record (CompiledScene::ctab)
 // against the capsule of radius rho around the segment [a, b] (u = b - a).
@@ -1618,7 +1638,7 @@ __device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, c
 // reach, then each surviving chunk runs the object test below.  Occlusion is
 // an OR over objects, so the order is free.
 template <bool EAGER, bool DEEP, bool UO, bool BV = false, class CT>
-__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin, real tmax, bool need, bool wave_ok,
+__device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
 #if defined(RT_ABL) && RT_ABL == 1   // diagnostic ablation builds only (wrong images): no shadow queries
     return false;
@@ -1677,7 +1697,11 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
                 const bool pass = (c < nch) & record_touch(k0, k1, K);
                 cm = (cap && exec_full()) ? __ballot(pass) : ~0ull;
             }
-            if (!((cm >> (ch & 63)) & 1ull)) continue;
+            if (!((cm >> (ch & 63)) & 1ull)) {
+                if constexpr (!std::is_same<CT, Cnt<false>>::value)
+                    if (need) cnt_add(cnt, RT_OPC_CULLED, chunk_objects(S, ch << 6));
+                continue;
+            }
         }
         const int base = ch << 6;
         const int nc = S.n_objs - base;
@@ -1756,6 +1780,343 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
             }
             if (S.cull && ob.has_bound) {   // per-lane segment test (f32, cheaper than an FP64 miss)
                 if (!__any(need && !hit && ball_touch(ob.fb, fr, ftmin, ftmax))) {
+                    if (need) cnt.inc(RT_OPC_CULLED);
+                    cnt.pe(PH_OBJ_PREF);
+                    continue;
+                }
+            }
+            cnt.pe(PH_OBJ_PREF);
+#if defined(RT_ABL) && RT_ABL == 3   // diagnostic: everything but the shadow object evaluations
+            if (m != 12345) continue;
+#endif
+            const bool csg_obj = ob.kind == rtamd::OBJ_CHAIN && ob.core != 0;
+            if (csg_obj) cnt.pb(PH_SHADOW_CSG);
+            cnt.pb(PH_OBJ_HIT);
+            cnt.ev(EV_SH_HIT);
+            if (csg_obj) cnt.ev(EV_SH_CSG);
+            if (!r_exact) {   // Ray::Ray (core.h:278) of the shadow ray (shading.cpp:98), in place
+                r.d = normalized(r.d);
+                r_exact = true;
+            }
+            {
+                // every lane evaluates (the wave runs the object anyway) and
+                // only querying lanes without a hit take the result: no
+                // divergent region between this loop's wave-wide tests.  The
+                // op-counting builds take the same path and count only the
+                // reference's calls (querying lanes without a hit yet).
+                real t = RV(0.0), ts = RV(0.0);
+                V3 p;
+                int code = 0;
+                const bool take = need && !hit;
+                cnt.gate(take);
+                const bool h = object_hit<EAGER, DEEP>(S, ob, r, tmin, tmax, t, p, ts, code, cnt, lmask, use_mask);
+                cnt.gate(true);
+                hit = hit || (take && h);
+            }
+            cnt.pe(PH_OBJ_HIT);
+            if (csg_obj) cnt.pe(PH_SHADOW_CSG);
+            if (__all(hit || !need)) return hit;
+        }
+    }
+    return hit;
+}
+
+
+// ------------------------------------------------ light-centred shadow culls
+// (the wave-BVH kernels: scenes of many objects, where the per-object cost of
+// the transposed test dominates).  Every shadow segment of one light ends at
+// that light (shading.cpp:79-104): lane i's ray starts at o_i = p_i + n_i
+// eps_i toward wi_i = (L - p_i) / dist_i and runs over t in (eps_i, dist_i -
+// eps_i), so each of its points (p_i + t wi_i) + n_i eps_i lies within eps_i
+// of the segment [L, p_i].  When every querying lane's hit point lies within
+// rho of q (ShadowHull, once per shade() call: q halfway between the first
+// querying lane's hit point and the one farthest from it), all of a wave's
+// segments for light L lie within emax (the largest eps) of the hull of L
+// and the ball B(q, rho): the cone from L with axis a = (q - L) / |q - L| and
+// half-angle asin(rho / |q - L|), cut at the ball.  The cull records are
+// light-relative and computed once per scene on the host
+// (CompiledScene::lrec / lgb: w = c - L and |w|^2 of each ball), so a
+// record's transposed test is one dot product and a few compares.  The
+// per-lane test of a surviving candidate stays ball_touch on the lane's
+// actual segment (its eps offset is what clears the object the lane itself
+// lies on); a bare half-space that passes the hull test (hit points on its
+// own plane) gets a per-lane test of the segment's start against its plane.
+// Conservative in f32 (margins of >= 1e-6 of the magnitudes involved); a wave
+// whose hull is not valid (a hit point within 0.1 of the light, where the
+// reference clamps the distance, or L inside the hull ball) tests every
+// object per lane instead.  Measured against the capsule (profiles/r04_*):
+// 4096 random spheres 52.0 -> 41.7 ms, the 576-sphere lattice 7.10 -> 4.88
+// ms, paper mode 24.7 -> 19.2 ms; on config 4 / 5 (15 / 65 objects) the
+// capsule's per-query setup is no dearer and it needs fewer registers, so the
+// kernels without the BVH keep it.
+struct ShadowHull {
+    float qx, qy, qz, rho, emax;
+    bool ok;
+};
+template <bool UO>
+__device__ __forceinline__ ShadowHull shadow_hull(const V3& p, real eps, bool valid, bool wave_ok) {
+    ShadowHull H{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, false};
+    const float px = (float)p.x, py = (float)p.y, pz = (float)p.z;
+    const uint64_t vm = __ballot(valid);
+    const bool full = wave_ok && exec_full();
+    const int f = vm ? __builtin_ctzll(vm) : 0;
+    H.qx = rdlane_f(px, f);
+    H.qy = rdlane_f(py, f);
+    H.qz = rdlane_f(pz, f);
+    const float e = valid ? (float)eps : 0.0f;
+    const bool bad = valid && !__builtin_isfinite(px + py + pz);
+    if (full && vm && !__any(bad)) {
+        // centre: halfway between lane f's hit point and the one farthest
+        // from it (about half the radius a corner lane's ball would have)
+        float dx = px - H.qx, dy = py - H.qy, dz = pz - H.qz;
+        const float d2f = valid ? __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)) : 0.0f;
+        const uint32_t mf = wave_max_u32(__float_as_uint(d2f));
+        const uint64_t gm = __ballot(valid && __float_as_uint(d2f) == mf);
+        const int g = gm ? __builtin_ctzll(gm) : f;
+        H.qx = uni<UO>(0.5f * (H.qx + rdlane_f(px, g)));
+        H.qy = uni<UO>(0.5f * (H.qy + rdlane_f(py, g)));
+        H.qz = uni<UO>(0.5f * (H.qz + rdlane_f(pz, g)));
+        dx = px - H.qx, dy = py - H.qy, dz = pz - H.qz;
+        const float d2 = valid ? __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)) : 0.0f;
+        H.rho = uni<UO>(sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(d2)))));
+        H.emax = uni<UO>(__uint_as_float(wave_max_u32(__float_as_uint(e))) * 1.000001f);
+        H.ok = __builtin_isfinite(H.rho);
+    }
+    return H;
+}
+
+// One light's cone over a ShadowHull (wave-uniform): axis a, cos / sin of
+// the half-angle beta, the hull ball's distance dq along the axis and radius
+// rho; beyond dq the hull is inside the cylinder of radius rend = rho / cb
+// up to xe = dq + rho.
+struct LightCone {
+    float ax, ay, az, cb, sb, dq, xe, rend, rho, emax, qx, qy, qz, mq;
+};
+
+// Ball record (w = c - L, |w|^2), (type, r, |w|_1 + r) against the hull: the
+// ball grown by emax (r') touches it only if L lies in it, or, with x the
+// axial and p the perpendicular coordinate of w: for x < dq (the cone
+// body) p cos(beta) <= r' + max(x, 0) sin(beta) and x >= -r'; for x >= dq
+// (the end) max(0, x - xe)^2 + max(0, p - rend)^2 <= r'^2.
+__device__ __forceinline__ bool lrec_ball_cone(const float4 c0, float r, float magw, const LightCone& K) {
+    const float x = dot_pk(f2(c0.x, c0.y), c0.z, f2(K.ax, K.ay), K.az);
+    const float p2 = __builtin_fmaxf(0.0f, __builtin_fmaf(-x, x, c0.w));
+    const float mw = 4e-6f * magw;
+    const float re = r + K.emax + mw;
+    const float m2 = 1e-6f * magw * magw;   // (the rounding of W2 - x^2: <= 4e-7 magw^2)
+    const float re2 = __builtin_fmaf(re, re, m2);
+    const float rhs = __builtin_fmaf(__builtin_fmaxf(x, 0.0f), K.sb, re);
+    const bool inside = !(c0.w > re2);
+    const bool body = !(p2 * (K.cb * K.cb) > __builtin_fmaf(rhs, rhs, m2)) & !(x < -re - mw);
+    const float ex = __builtin_fmaxf(0.0f, x - K.xe);
+    const float ep = __builtin_fmaxf(0.0f, sqrt_cull(p2) - K.rend - mw);
+    const bool end = !(__builtin_fmaf(ex, ex, ep * ep) > re2);
+    return inside | ((x < K.dq) ? body : end);   // NaN passes
+}
+
+// Lane j's transposed test of its light-relative record (types: 0 never,
+// 1 always, 2 ball, 3 bare half-space plane (n, n.p), (type, n.L - n.p, mag)).
+__device__ __forceinline__ bool lrec_touch(const float4 c0, const float4 c1, const LightCone& K) {
+    const int type = __float_as_int(c1.x);
+    const bool ball = lrec_ball_cone(c0, c1.y, c1.z, K);
+    // a plane: every segment point's signed distance lies between the
+    // light's (c1.y) and its hit point's (within rho of q's) +- emax
+    const float sq = dot_pk(f2(c0.x, c0.y), c0.z, f2(K.qx, K.qy), K.qz) - c0.w;
+    const float mp = 1e-5f * (c1.z + K.mq + K.rho) + K.emax;
+    const float sl = c1.y;
+    const bool plane = !((sl > mp) & (sq - K.rho > mp)) & !((sl < -mp) & (sq + K.rho < -mp));   // NaN passes
+    return (type == 1) | ((type == 2) & ball) | ((type == 3) & plane);
+}
+
+// A world ball (c, r) (wave BVH chunk records) against the cone, made
+// light-relative on the fly.
+__device__ __forceinline__ bool ball_cone(const float4 g, const LightCone& K, float Lx, float Ly, float Lz) {
+    const float wx = g.x - Lx, wy = g.y - Ly, wz = g.z - Lz;
+    const float w2 = __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz));
+    const float magw = __builtin_fabsf(wx) + __builtin_fabsf(wy) + __builtin_fabsf(wz) + g.w;
+    return lrec_ball_cone(make_float4(wx, wy, wz, w2), g.w, magw, K);
+}
+
+// Scene::occluded (scene.cpp:33-42) for the querying lanes of a fully active
+// wave, light li of S.lights.  Returns false for lanes with need = false.
+//
+// r0 is the shadow ray BEFORE the Ray constructor's re-normalisation of its
+// direction (core.h:278; r0.d = wi, unit for every lane whose light distance
+// was not clamped, regular = d2 > 0.01): the culls work on it directly, and
+// the exact FP64 ray (make_ray, one sqrt and three divisions per lane) is
+// formed only when some candidate object survives them and is evaluated -
+// most shadow queries of a wave end before that.
+//
+// BV (wave BVH kernels): S.objs is the Morton-ordered list in chunks of 64
+// with a cull record per chunk (CompiledScene::wobjs / wchunk); one
+// transposed test per 64 chunks skips every chunk no querying segment can
+// reach, then each surviving chunk runs the object test below.  Occlusion is
+// an OR over objects, so the order is free.
+template <bool EAGER, bool DEEP, bool UO, bool BV = false, class CT>
+__device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin, real tmax, bool need, bool wave_ok,
+                                    CT& cnt, int li, const ShadowHull& H, bool regular) {
+#if defined(RT_ABL) && RT_ABL == 1   // diagnostic ablation builds only (wrong images): no shadow queries
+    return false;
+#endif
+    cnt.pb(PH_WAVE_SETUP);
+    DRay r = r0;           // the exact ray, formed on the first object evaluation (wave-uniform)
+    bool r_exact = false;
+    const uint64_t nm = __ballot(need);
+    if (!nm) return false;
+    cnt.ev(EV_SHQ);
+    const int f = __builtin_ctzll(nm);
+    const LightT* Lp = &S.lights[li];
+    const float Lx = (float)Lp->pos[0], Ly = (float)Lp->pos[1], Lz = (float)Lp->pos[2];
+    // the light's cone over the shade call's hull (uniform; shadow_hull)
+    LightCone K;
+    bool cone = H.ok && wave_ok && exec_full() && !__any(need && !regular);
+    {
+        const float dx = H.qx - Lx, dy = H.qy - Ly, dz = H.qz - Lz;
+        const float dq = sqrt_cull(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+        const float mq = __builtin_fabsf(H.qx) + __builtin_fabsf(H.qy) + __builtin_fabsf(H.qz) + __builtin_fabsf(Lx) +
+                         __builtin_fabsf(Ly) + __builtin_fabsf(Lz);
+        const float rho = __builtin_fmaf(H.rho, 1.00001f, 1e-6f * (mq + 1.0f));
+        const float inv = __builtin_amdgcn_rcpf(dq);
+        const float sb = __builtin_fminf(1.0f, rho * inv * 1.00001f + 1e-6f);
+        const float cb = sqrt_cull(__builtin_fmaxf(0.0f, __builtin_fmaf(-sb, sb, 1.0f))) * 0.99999f - 1e-6f;
+        cone = cone && (dq > rho * 1.0001f) && (cb > 0.0f);
+        K.ax = uni<UO>(dx * inv), K.ay = uni<UO>(dy * inv), K.az = uni<UO>(dz * inv);
+        K.cb = uni<UO>(cb), K.sb = uni<UO>(sb);
+        K.dq = uni<UO>(dq * 0.99999f);
+        K.xe = uni<UO>((dq + rho) * 1.00001f);
+        K.rend = uni<UO>(rho * __builtin_amdgcn_rcpf(cb) * 1.00001f + 1e-6f * mq);
+        K.rho = uni<UO>(rho), K.emax = H.emax;
+        K.qx = H.qx, K.qy = H.qy, K.qz = H.qz;
+        K.mq = uni<UO>(mq);
+    }
+    const float leps = (float)tmin * 1.0000002f;
+    const int lane = __lane_id();
+    const float4* lrec = S.lrec + 2 * (size_t)li * S.n_objs;
+    const float4* lgb = S.lgb + 2 * (size_t)li * S.n_gb;
+    // line bundle for the CSG leaf masks, built on first use (cone only)
+    bool lb_ready = false;
+    Cone LB{f2(0.0f, 0.0f), f2(0.0f, 0.0f), 0.0f, 0.0f, -1.0f, 1.0f, 0.0f, 0.0f};
+    bool hit = false;
+    const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
+    uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 some querying segment can reach
+    for (int ch = 0; ch < nch; ++ch) {
+        if constexpr (BV) {
+            if ((ch & 63) == 0) {
+                const int c = ch + lane;
+                const int cr = c < nch ? c : nch - 1;
+                const float4 k0 = S.wchunk[2 * cr], k1 = S.wchunk[2 * cr + 1];
+                const int ktype = __float_as_int(k1.x);
+                const bool pass = (c < nch) & ((ktype != 2) | ball_cone(k0, K, Lx, Ly, Lz));
+                cm = (cone && exec_full()) ? __ballot(pass) : ~0ull;
+            }
+            if (!((cm >> (ch & 63)) & 1ull)) {
+                if constexpr (!std::is_same<CT, Cnt<false>>::value)
+                    if (need) cnt_add(cnt, RT_OPC_CULLED, chunk_objects(S, ch << 6));
+                continue;
+            }
+        }
+        const int base = ch << 6;
+        const int nc = S.n_objs - base;
+        const int j = base + lane;
+        // the object's light-relative record (CompiledScene::lrec): one
+        // 32-byte load on every lane (lanes past the last object re-read it
+        // and are masked)
+        const int jr = j < S.n_objs ? j : S.n_objs - 1;
+        const float4 c0 = lrec[2 * jr], c1 = lrec[2 * jr + 1];
+        const bool pass = (j < S.n_objs) & (cone ? lrec_touch(c0, c1, K) : __float_as_int(c1.x) != 0);
+        // (lane j tests object j only with the whole wave active; otherwise
+        // every object of the chunk is a candidate)
+        uint64_t m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        cnt.pe(PH_WAVE_SETUP);
+#if defined(RT_ABL) && RT_ABL == 2   // diagnostic: setup + transposed test only
+        if (m != 12345) return false;
+#endif
+        if constexpr (!std::is_same<CT, Cnt<false>>::value) {
+            if (need) {
+                int skipped = 0;
+                for (int o = base; o < S.n_objs && o < base + 64; ++o) {
+                    const int k = S.objs[o].kind;
+                    if (k != rtamd::OBJ_GROUP && k != rtamd::OBJ_NEVER && !((m >> (o - base)) & 1)) ++skipped;
+                }
+                cnt_add(cnt, RT_OPC_CULLED, skipped);
+            }
+        }
+        while (m) {
+            const int o = base + __builtin_ctzll(m);
+            m &= m - 1;
+            const DevObj ob = S.objs[o];
+            if (ob.kind == rtamd::OBJ_GROUP || ob.kind == rtamd::OBJ_NEVER) continue;
+            cnt.ev(EV_SH_CAND);
+            cnt.pb(PH_OBJ_PREF);
+            // CSG objects: no lane's segment reaches a leaf ball (DevObj::pb0);
+            // otherwise the leaves whose balls no querying lane's line meets
+            uint64_t lmask = ~0ull;
+            bool use_mask = false;
+            if (cone && ob.npb > 0 && exec_full()) {
+                const int k = ob.pb0 + (lane < ob.npb ? lane : 0);
+                const float4 g0 = lgb[2 * k], g1 = lgb[2 * k + 1];
+                const bool in = lane < ob.npb;
+                if (!__any(in && lrec_ball_cone(g0, g1.y, g1.z, K))) {
+                    if (need) cnt.inc(RT_OPC_CULLED);
+                    cnt.pe(PH_OBJ_PREF);
+                    continue;
+                }
+                if (!lb_ready) {
+                    // line bundle of the querying lanes (lane f's line as the axis)
+                    lb_ready = true;
+                    const FRay fr = to_fray(r0);
+                    const float lox = rdlane_f(fr.ox, f), loy = rdlane_f(fr.oy, f), loz = rdlane_f(fr.oz, f);
+                    const float lax = rdlane_f(fr.dx, f), lay = rdlane_f(fr.dy, f), laz = rdlane_f(fr.dz, f);
+                    const float dxo = fr.ox - lox, dyo = fr.oy - loy, dzo = fr.oz - loz;
+                    const float do2 = need ? dxo * dxo + dyo * dyo + dzo * dzo : 0.0f;
+                    const float dc = need ? __builtin_fmaxf(0.0f, 1.0f - __builtin_fmaf(fr.dx, lax, __builtin_fmaf(fr.dy, lay, fr.dz * laz)))
+                                          : 0.0f;
+                    const float lrho = uni<UO>(sqrt_cull(__uint_as_float(wave_max_u32(__float_as_uint(do2)))));
+                    const float dcm = __uint_as_float(wave_max_u32(__float_as_uint(dc))) + 4e-6f;
+                    const float lcth = uni<UO>(1.0f - dcm);
+                    LB.oxy = f2(lox, loy), LB.axy = f2(lax, lay), LB.oz = loz, LB.az = laz;
+                    LB.cth = lcth;
+                    LB.sth = uni<UO>(sqrt_cull(__builtin_fmaxf(0.0f, 1.0f - lcth * lcth)) + 1e-6f);
+                    LB.rho = lrho;
+                    LB.m5 = uni<UO>(1e-5f * (__builtin_fabsf(lox) + __builtin_fabsf(loy) + __builtin_fabsf(loz) + lrho + 1.0f));
+                }
+#ifdef RT_NO_LEAF_MASK
+                use_mask = false;
+#else
+                use_mask = LB.cth > 0.0f;
+#endif
+                if (use_mask) {
+                    const bool full = exec_full();
+                    const uint64_t b = __ballot(in && line_touch(S.gb + 4 * k, LB));
+                    lmask = full ? b : ~0ull;
+                }
+            }
+            if (cone && ob.kind == rtamd::OBJ_HALF) {
+                // a bare half-space passed the hull test (hit points on or
+                // near its plane: the hull cannot tell their sides, the
+                // segments can): lane i's segment runs from A_i = o_i + tmin
+                // d_i to within 2 eps of L, so it crosses the plane only if
+                // A_i's signed distance and the light's (record) allow it
+                const float4 o0 = lrec[2 * o], o1 = lrec[2 * o + 1];   // (n, n.p), (type, n.L - n.p, mag)
+                const float ax = (float)__builtin_fma(tmin, r0.d.x, r0.o.x), ay = (float)__builtin_fma(tmin, r0.d.y, r0.o.y),
+                            az = (float)__builtin_fma(tmin, r0.d.z, r0.o.z);
+                const float sa = dot_pk(f2(o0.x, o0.y), o0.z, f2(ax, ay), az) - o0.w;
+                const float mp = 1e-5f * (o1.z + __builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az));
+                const float e2 = 2.0f * leps;   // (the far end: within 2 eps of L)
+                const float sl = o1.y;
+                const bool cross = !((sa > mp) & (sl - e2 > mp)) & !((sa < -mp) & (sl + e2 < -mp));   // NaN passes
+                if (!__any(need && !hit && cross)) {
+                    if (need) cnt.inc(RT_OPC_CULLED);
+                    cnt.pe(PH_OBJ_PREF);
+                    continue;
+                }
+            }
+            if (S.cull && ob.has_bound) {
+                // per-lane segment test (f32, cheaper than an FP64 miss) on the
+                // lane's actual segment: its eps offset from the hit point is
+                // what clears the object a lane itself lies on
+                const FRay fr = to_fray(r0);
+                if (!__any(need && !hit && ball_touch(ob.fb, fr, (float)tmin, (float)tmax))) {
                     if (need) cnt.inc(RT_OPC_CULLED);
                     cnt.pe(PH_OBJ_PREF);
                     continue;
@@ -1878,7 +2239,11 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 const bool pass = (c < nch) & ((ktype != 2) | wide | cone_touch(k0, k1.y, K));
                 cm = (cone && exec_full()) ? __ballot(pass) : ~0ull;
             }
-            if (!((cm >> (ch & 63)) & 1ull)) continue;
+            if (!((cm >> (ch & 63)) & 1ull)) {
+                if constexpr (!std::is_same<CT, Cnt<false>>::value)
+                    if (valid) cnt_add(cnt, RT_OPC_CULLED, chunk_objects(S, ch << 6));
+                continue;
+            }
         }
         const int base = ch << 6;
         const int j = base + lane;
@@ -2060,6 +2425,10 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
     const bool wave_full = WV && __builtin_amdgcn_read_exec() == ~0ull;
     const V3 n = hit.n;
     const real eps = cmax(RV(1e-3), RV(1e-4) * ht);   // (no zeros)
+    // the wave's hit points once per call: the light-centred shadow culls
+    // of every light start from them (scene_occluded_wave)
+    ShadowHull hull{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, false};
+    if constexpr (WV == 2) hull = shadow_hull<UO>(hit.p, eps, valid, wave_full);
     // Two passes over the lights so that only (p, n, eps) stay live across
     // the shadow queries (register pressure): pass 1 decides, per light, the
     // reference's early-outs and the occlusion query; pass 2 recomputes the
@@ -2129,10 +2498,15 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             cnt.ev(EV_LIGHT1);
             const V3 so = v3(hit.p.x + n.x * eps, hit.p.y + n.y * eps, hit.p.z + n.z * eps);
             bool occ = false;
-            if constexpr (WV) {
+            if constexpr (WV == 2) {
                 cnt.pb(PH_SHADOW);
                 // (the direction's re-normalisation happens inside, when needed)
-                occ = scene_occluded_wave<EAGER, DEEP, UO, (WV == 2)>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
+                occ = scene_occluded_wave<EAGER, DEEP, UO, true>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt, li,
+                                                                 hull, d2 > RV(0.01));
+                cnt.pe(PH_SHADOW);
+            } else if constexpr (WV) {
+                cnt.pb(PH_SHADOW);
+                occ = scene_occluded_capsule<EAGER, DEEP, UO, false>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
                 cnt.pe(PH_SHADOW);
             } else {
                 const DRay sr = make_ray(so, wi);

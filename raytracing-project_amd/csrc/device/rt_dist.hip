@@ -1,13 +1,15 @@
 // rt_dist.hip — frames on several GPUs and the device output path.
 //
 // pixels are independent, so a frame is partitioned by OUTPUT
-// ROWS: strip s of RT_STRIP_ROWS rows (paper mode: RT_PAPER_STRIP_ROWS) goes
-// to rank s mod N (interleaving balances cheap sky rows against expensive
-// geometry rows).  Every rank runs
+// ROWS: strips of RT_STRIP_ROWS rows (paper mode: RT_PAPER_STRIP_ROWS) are
+// dealt to the ranks interleaved (strip_owners: balances cheap sky rows
+// against expensive geometry rows).  Every rank runs
 // the ordinary trace (rt_frame_* of rt_render.hip) on its rows, chunk by
 // chunk, and each chunk is handed to ONE RCCL collective, ncclGather to rank
 // 0 over xGMI, on a high-priority stream so it overlaps the tracing of the
-// next chunk; rank 0 places the gathered strips into its frame.  The jitter
+// next chunk; rank 0 places the gathered strips into its frame.  Paper-mode
+// ranks gather one byte per pixel (the output alphabet, paper_code_value),
+// which rank 0 decodes into its FP64 or RGB8 frame.  The jitter
 // stream of every row is taken at that row's own stream offset, so the frame
 // is bit-identical to a one-GPU render (tracer.cpp:284-299).
 //
@@ -92,18 +94,53 @@ struct DevBuf {
 // rows and waves straddling strips 16+ rows apart).
 int strip_height(int mode) { return mode == RT_MODE_PAPER ? RT_PAPER_STRIP_ROWS : RT_STRIP_ROWS; }
 
-std::vector<int32_t> strip_rows(int H, int world, int rank, int S = RT_STRIP_ROWS) {
-    std::vector<int32_t> rows;
-    for (int s = 0; s * S < H; ++s)
-        if (s % world == rank)
-            for (int r = s * S; r < std::min(H, (s + 1) * S); ++r) rows.push_back(r);
-    return rows;
+// Which rank renders strip s.  Interleaved so that every rank samples the
+// whole frame (cheap sky rows against expensive geometry rows), by a smooth
+// weighted round robin: every strip, each rank's credit grows by its weight
+// and the rank with the most credit takes the strip (and pays the total).
+//  * Ties go to the rank first in a per-round rotation (round k = strips
+//    [k*world, (k+1)*world) starts at rank k mod world), so a rank's strips do
+//    not all sit at the same phase of a world*S-row period: config 5's sphere
+//    rows have structure on that scale (a plain s mod world split left the
+//    slowest of 8 paper-mode ranks 11 % above the mean).
+//  * Rank 0 also places every gathered strip into the frame (the FP64 frame:
+//    24 B/px written; paper mode decodes one byte per pixel into 24), so it
+//    renders fewer strips: weight 1 - c*world (per mille: c = 30 paper, 8
+//    standard, 0 for RGB8 output; from per-rank timings, profiles/r04*).
+// The partition is a pure function of (H, world, mode, kind), all of which
+// the ranks check against each other before the first gather.
+constexpr int kRootShedPaper = 30, kRootShedStd = 8;
+std::vector<int> strip_owners(int n_strips, int world, int mode, int kind) {
+    std::vector<int> own((size_t)std::max(0, n_strips), 0);
+    if (world <= 1) return own;
+    std::vector<int64_t> w((size_t)world, 1000), cur((size_t)world, 0);
+    const int64_t c = kind ? 0 : (mode == RT_MODE_PAPER ? kRootShedPaper : kRootShedStd);
+    w[0] = std::max<int64_t>(500, 1000 - c * world);
+    int64_t total = 0;
+    for (int64_t v : w) total += v;
+    for (int s = 0; s < n_strips; ++s) {
+        for (int r = 0; r < world; ++r) cur[r] += w[r];
+        const int rot = (s / world) % world;
+        int best = rot;
+        for (int i = 1; i < world; ++i) {
+            const int r = (rot + i) % world;
+            if (cur[r] > cur[best]) best = r;
+        }
+        own[s] = best;
+        cur[best] -= total;
+    }
+    return own;
 }
 
-int max_rows(int H, int world, int S = RT_STRIP_ROWS) {
-    int m = 0;
-    for (int r = 0; r < world; ++r) m = std::max(m, (int)strip_rows(H, world, r, S).size());
-    return m;
+// Output rows of every rank (ascending per rank), strips of strip_height(mode).
+std::vector<std::vector<int32_t>> partition_rows(int H, int world, int mode, int kind) {
+    const int S = strip_height(mode);
+    const int n_strips = (H + S - 1) / S;
+    const std::vector<int> own = strip_owners(n_strips, world, mode, kind);
+    std::vector<std::vector<int32_t>> rows((size_t)world);
+    for (int st = 0; st < n_strips; ++st)
+        for (int r = st * S; r < std::min(H, (st + 1) * S); ++r) rows[own[st]].push_back(r);
+    return rows;
 }
 
 // `chunks` contiguous pieces of [0, m), each a whole number of strips of S
@@ -329,6 +366,16 @@ __global__ void k_test_stall(unsigned long long max_ticks) {
 
 enum { kInjectTraceFail = 1, kInjectStall = 2 };
 
+// Row chunks per rank and frame (each one gather): kChunks, or
+// RT_DIST_CHUNKS (standard mode) / RT_DIST_CHUNKS_PAPER from the environment
+// (measurement A/B; 1 .. kChunks).
+int frame_chunks(int mode) {
+    static const int c[2] = {
+        [] { const char* e = std::getenv("RT_DIST_CHUNKS"); return e && *e ? std::atoi(e) : kChunks; }(),
+        [] { const char* e = std::getenv("RT_DIST_CHUNKS_PAPER"); return e && *e ? std::atoi(e) : kChunks; }()};
+    return std::min(kChunks, std::max(1, c[mode == RT_MODE_PAPER ? 1 : 0]));
+}
+
 // RT_DIST_TIMEOUT_MS: how long a rank waits for its peers inside one frame
 // before it aborts the communicator (default 120 s).
 double env_timeout_ms() {
@@ -376,15 +423,17 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     }
     const int Wc = std::max(W, 1), Hc = std::max(H, 1);
     const int S = strip_height(mode == RT_MODE_PAPER ? RT_MODE_PAPER : RT_MODE_STANDARD);
-    const std::vector<int32_t> rows = strip_rows(Hc, D.world, D.rank, S);
+    const std::vector<std::vector<int32_t>> part = partition_rows(Hc, D.world, mode, kind);
+    const std::vector<int32_t>& rows = part[D.rank];
     const int n = (int)rows.size();
-    const int m = max_rows(Hc, D.world, S);
+    int m = 0;
+    for (const auto& pr : part) m = std::max(m, (int)pr.size());
     const size_t row_elems = (size_t)Wc * 3;
     // paper mode (FP64) across ranks: each rank produces one paper-code byte
     // per pixel, 1 B/px crosses xGMI, and the root decodes (k_place_codes)
     const bool codes = coll && mode == RT_MODE_PAPER && !(flags & RT_FLAG_FP32);
     const size_t row_bytes = codes ? (size_t)Wc : row_elems * (kind ? 1 : sizeof(double));   // gathered per row
-    const auto bounds = chunk_bounds(m, coll ? kChunks : 1, S);
+    const auto bounds = chunk_bounds(m, coll ? frame_chunks(mode) : 1, S);
     const bool direct = !coll && kind == 0;   // trace straight into the caller's frame
     DevBuf& stage = D.sim_stage ? *D.sim_stage : D.stage;
     auto fail = [&](int code, const char* what) {
@@ -405,7 +454,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         // placement table: chunk k occupies slots [world*a, world*b) as [rank][b-a]
         D.rowtab_host.assign((size_t)D.world * m, -1);
         for (int r = 0; r < D.world; ++r) {
-            const std::vector<int32_t> rr = strip_rows(H, D.world, r, S);
+            const std::vector<int32_t>& rr = part[r];
             for (const auto& ab : bounds)
                 for (int i = ab.first; i < ab.second; ++i)
                     D.rowtab_host[(size_t)D.world * ab.first + (size_t)r * (ab.second - ab.first) + (i - ab.first)] =
@@ -803,7 +852,7 @@ extern "C" int rt_dist_rows_mode(int H, int world, int rank, int mode, int32_t* 
     if (H <= 0 || world <= 0 || rank < 0 || rank >= world || !rows_out ||
         (mode != RT_MODE_STANDARD && mode != RT_MODE_PAPER))
         return RT_ERR_INVALID_ARG;
-    const std::vector<int32_t> r = strip_rows(H, world, rank, strip_height(mode));
+    const std::vector<int32_t> r = partition_rows(H, world, mode, 0)[rank];
     std::copy(r.begin(), r.end(), rows_out);
     return (int)r.size();
 }

@@ -340,6 +340,9 @@ DevScene make_scene(const SceneView& V, bool bv = false) {
     S.ops = V.ops;
     S.gb = V.gb;
     S.ctab = reinterpret_cast<const float4*>(bv ? V.wctab : V.ctab);
+    S.lrec = reinterpret_cast<const float4*>(bv ? V.lwrec : V.lrec);
+    S.lgb = reinterpret_cast<const float4*>(V.lgb);
+    S.n_gb = V.n_gb;
     S.fold = static_cast<const FoldT*>(V.fold);
     S.worig = bv ? V.worig : nullptr;
     S.wchunk = reinterpret_cast<const float4*>(bv ? V.wchunk : nullptr);

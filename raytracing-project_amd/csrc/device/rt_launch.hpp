@@ -70,6 +70,10 @@ struct SceneView {
     const DevOp* ops;
     const float* gb;
     const float* ctab;   // CompiledScene::ctab
+    const float* lrec;   // CompiledScene::lrec / lwrec / lgb: light-relative shadow cull records
+    const float* lwrec;
+    const float* lgb;
+    int n_gb;
     const void* fold;   // FoldLeafR of the launching precision
     // wave BVH (CompiledScene::wobjs, wctab, worig, wchunk); n_chunks = 0: none
     const DevObj* wobjs;

@@ -118,7 +118,7 @@ struct SceneCache {
 // Per-device workspace (one render at a time per device; guarded by a mutex).
 struct Workspace {
     std::mutex mu;
-    DBuf nodes, mats, lights, dlights, objs, ops, gb, ctab;
+    DBuf nodes, mats, lights, dlights, objs, ops, gb, ctab, lrec, lwrec, lgb;
     DBuf wobjs, wctab, worig, wchunk;   // wave BVH (CompiledScene::wobjs ...)
     DBuf fold;
     DBuf nodes_f, mats_f, lights_f, dlights_f, fold_f;   // float copies (RT_FLAG_FP32)
@@ -321,6 +321,9 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(upload(ws.ops, sc.cs.ops, st));
         HIP_TRY(upload(ws.gb, sc.cs.gbounds, st));
         HIP_TRY(upload(ws.ctab, sc.cs.ctab, st));
+        HIP_TRY(upload(ws.lrec, sc.cs.lrec, st));
+        HIP_TRY(upload(ws.lwrec, sc.cs.lwrec, st));
+        HIP_TRY(upload(ws.lgb, sc.cs.lgb, st));
         HIP_TRY(upload(ws.wobjs, sc.cs.wobjs, st));
         HIP_TRY(upload(ws.wctab, sc.cs.wctab, st));
         HIP_TRY(upload(ws.worig, sc.cs.worig, st));
@@ -386,6 +389,10 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.ops = ws.ops.as<rtamd::DevOp>();
     S.gb = ws.gb.as<float>();
     S.ctab = ws.ctab.as<float>();
+    S.lrec = ws.lrec.as<float>();
+    S.lwrec = ws.lwrec.as<float>();
+    S.lgb = ws.lgb.as<float>();
+    S.n_gb = (int)(sc.cs.gbounds.size() / 4);
     S.wobjs = ws.wobjs.as<rtamd::DevObj>();
     S.wctab = ws.wctab.as<float>();
     S.worig = ws.worig.as<int32_t>();
@@ -712,7 +719,8 @@ int rtamd::release_device_workspaces() {
         std::lock_guard<std::mutex> wl(w->mu);   // waits for an open frame of this device
         (void)hipSetDevice((int)dev);
         (void)hipDeviceSynchronize();
-        for (DBuf* b : {&w->nodes, &w->mats, &w->lights, &w->dlights, &w->objs, &w->ops, &w->gb, &w->ctab, &w->fold,
+        for (DBuf* b : {&w->nodes, &w->mats, &w->lights, &w->dlights, &w->objs, &w->ops, &w->gb, &w->ctab, &w->lrec,
+                        &w->lwrec, &w->lgb, &w->fold,
                         &w->wobjs, &w->wctab, &w->worig, &w->wchunk,
                         &w->nodes_f, &w->mats_f, &w->lights_f, &w->dlights_f, &w->fold_f, &w->rows, &w->jit, &w->ckpt,
                         &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb})

@@ -68,6 +68,40 @@ float float_ball_mag(const float b[4]) {
     return std::nextafter((float)m, INFINITY);
 }
 
+// Light-relative shadow cull records (CompiledScene::lrec / lwrec / lgb):
+// for every point light L, one 8-float record per input record (ctab layout:
+// c0 = ball (c, r) or plane (n, n.p); c1.x = type; c1.y = magnitude).  A ball
+// becomes (w = c - L, |w|^2) + (type, r, |w.x|+|w.y|+|w.z|+r); a bare
+// half-space's plane (n, n.p) + (type, n.L - n.p, |p| + |L|); other types are
+// copied.  `stride` floats per input record (8 for ctab, 4 for bare balls of
+// gbounds, which are all type 2).  Computed in double, rounded to nearest:
+// the device tests carry margins of >= 4e-6 of these magnitudes.
+void light_records(const float* rec, size_t n, int stride, const rt_light* lights, int n_lights,
+                   std::vector<float>& out) {
+    out.assign((size_t)std::max(0, n_lights) * n * 8, 0.0f);
+    for (int l = 0; l < n_lights; ++l) {
+        const double* L = lights[l].pos;
+        for (size_t j = 0; j < n; ++j) {
+            const float* r = rec + (size_t)stride * j;
+            float* o = &out[((size_t)l * n + j) * 8];
+            int type = 2;
+            if (stride == 8) std::memcpy(&type, &r[4], sizeof(int));
+            if (type == 2) {
+                const double w[3] = {(double)r[0] - L[0], (double)r[1] - L[1], (double)r[2] - L[2]};
+                for (int k = 0; k < 3; ++k) o[k] = (float)w[k];
+                o[3] = (float)(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+                o[5] = r[3];
+                o[6] = std::nextafter((float)(std::fabs(w[0]) + std::fabs(w[1]) + std::fabs(w[2]) + (double)r[3]), INFINITY);
+            } else if (type == 3) {
+                for (int k = 0; k < 4; ++k) o[k] = r[k];
+                o[5] = (float)((double)r[0] * L[0] + (double)r[1] * L[1] + (double)r[2] * L[2] - (double)r[3]);
+                o[6] = std::nextafter((float)((double)r[5] + std::fabs(L[0]) + std::fabs(L[1]) + std::fabs(L[2])), INFINITY);
+            }
+            std::memcpy(&o[4], &type, sizeof(int));
+        }
+    }
+}
+
 bool is_degenerate_scaling(const rt_node& n) {
     const double kEPS = 1e-6;   // core.h:10, checked at transform.cpp:97
     return n.kind == RT_NODE_SCALING &&
@@ -469,6 +503,9 @@ public:
             std::memcpy(&c[4], &type, sizeof(int));
         }
         build_wave_bvh(cs);
+        light_records(cs.ctab.data(), cs.objs.size(), 8, d_.lights, d_.n_lights, cs.lrec);
+        light_records(cs.wctab.data(), cs.wobjs.size(), 8, d_.lights, d_.n_lights, cs.lwrec);
+        light_records(cs.gbounds.data(), cs.gbounds.size() / 4, 4, d_.lights, d_.n_lights, cs.lgb);
         return cs;
     }
 

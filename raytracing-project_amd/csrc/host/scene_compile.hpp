@@ -95,7 +95,7 @@ struct CompiledScene {
     std::vector<float> ctab;
     std::vector<float> gbounds;    // OP_IVL_GROUP bounds: (cx, cy, cz, r) per group, in the CSG frame, f32-inflated;
                                    // then the leaf prefilter balls of CHAIN objects (world frame, see DevObj::pb0)
-    // Wave BVH (scenes with more than kWaveChunk objects and no eager
+    // Wave BVH (scenes with more than kWaveBvhMin = 256 objects and no eager
     // programs; DESIGN.md §Wave BVH): the wave kernels' object list - every
     // object except group headers and never-hit objects, unbounded ones
     // first, the rest in Morton order of their bound centres - with its cull
@@ -107,6 +107,10 @@ struct CompiledScene {
     std::vector<float> wctab;
     std::vector<int32_t> worig;
     std::vector<float> wchunk;
+    // Light-relative shadow cull records (light_records, scene_compile.cpp):
+    // [light][record] x 8 floats for ctab (lrec), wctab (lwrec) and every
+    // gbounds ball (lgb); the shadow-query culls of scene_occluded_wave.
+    std::vector<float> lrec, lwrec, lgb;
     int max_ray_depth = 0;   // transform nesting on any path of an eager program (chains need no stack)
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter

@@ -1,7 +1,8 @@
 """Row-strip distribution of one frame over ranks.
 
-Each rank renders interleaved strips of STRIP output rows (strip s goes to rank
-s % world), which balances cheap sky rows against expensive geometry rows.
+Each rank renders interleaved strips of STRIP output rows (strip_owners: a
+weighted round robin rotated every round, the root lighter), which balances
+cheap sky rows against expensive geometry rows.
 All ranks' row buffers are padded to the same row count so one all_gather
 collects them; rank 0 then scatters the real rows into the frame.
 Used by bench.py (RCCL, device buffers) and tests/test_dist_gloo.py (gloo).
@@ -16,10 +17,44 @@ def strip_for(mode: int) -> int:
     return PAPER_STRIP if mode == 1 else STRIP
 
 
-def strip_rows(H: int, rank: int, world: int, strip: int = STRIP) -> list[int]:
+ROOT_SHED = {0: 8, 1: 30}   # per mille per rank of the root's weight (rt_dist.hip kRootShedStd / kRootShedPaper)
+
+
+def strip_owners(n_strips: int, world: int, mode: int = 0, kind: int = 0) -> list[int]:
+    """rt_dist.hip strip_owners: smooth weighted round robin over the strips,
+    ties to the rank first in a per-round rotation, the root's weight reduced
+    by ROOT_SHED[mode] per mille per rank (FP64 output) for its placement work."""
+    if world <= 1:
+        return [0] * n_strips
+    w = [1000] * world
+    w[0] = max(500, 1000 - (0 if kind else ROOT_SHED[1 if mode == 1 else 0]) * world)
+    total = sum(w)
+    cur = [0] * world
+    own = []
+    for s in range(n_strips):
+        for r in range(world):
+            cur[r] += w[r]
+        rot = (s // world) % world
+        best = rot
+        for i in range(1, world):
+            r = (rot + i) % world
+            if cur[r] > cur[best]:
+                best = r
+        own.append(best)
+        cur[best] -= total
+    return own
+
+
+def strip_rows(H: int, rank: int, world: int, strip: int = STRIP, mode: int | None = None, kind: int = 0) -> list[int]:
+    """Output rows rank renders (ascending): rt_dist_rows_mode's partition.
+    mode defaults to the one whose strip height `strip` is."""
+    if mode is None:
+        mode = 1 if strip == PAPER_STRIP else 0
+    n = (H + strip - 1) // strip
+    own = strip_owners(n, world, mode, kind)
     rows = []
-    for s in range((H + strip - 1) // strip):
-        if s % world == rank:
+    for s in range(n):
+        if own[s] == rank:
             rows.extend(range(s * strip, min(H, (s + 1) * strip)))
     return rows
 

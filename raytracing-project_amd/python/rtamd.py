@@ -219,14 +219,21 @@ def check_one_hip_runtime() -> str:
     first has torch's bundled runtime (same soname) already mapped, and
     librtamd.so binds to it; loading torch afterwards maps a second runtime
     (two runtimes torn down at exit aborted the process).  Raises in both
-    cases; returns the runtime's path."""
+    cases; a single runtime outside ROCM_PATH only warns.  Returns the
+    runtime's path."""
     hips = mapped_libraries("libamdhip64.so")
     if len(hips) > 1:
         raise RuntimeError("two HIP runtimes mapped in this process: " + ", ".join(hips) +
                            " (do not import torch in a process that uses librtamd.so)")
+    if hips and os.sep + "torch" + os.sep in hips[0]:
+        raise RuntimeError(f"librtamd.so is bound to torch's bundled HIP runtime {hips[0]} "
+                           "(import torch after, or not at all in, a process that uses librtamd.so)")
     if hips and not hips[0].startswith(ROCM_DIR + os.sep):
-        raise RuntimeError(f"librtamd.so is bound to the HIP runtime {hips[0]}, not {ROCM_DIR}'s "
-                           "(was torch imported first?)")
+        # one runtime, not a torch wheel's: another ROCm install (/opt/rocm-X.Y without the
+        # /opt/rocm link, a distro package) is legitimate
+        import warnings
+
+        warnings.warn(f"librtamd.so runs on the HIP runtime {hips[0]}, outside ROCM_PATH={ROCM_DIR}")
     return hips[0] if hips else ""
 
 

@@ -116,7 +116,7 @@ def cfg5_scene() -> dict:
 
 
 def bvh_scenes(dpi: int = 16) -> dict[str, dict]:
-    """Scenes of more than one wave's 64 objects, for the wave BVH
+    """Scenes of more than kWaveBvhMin = 256 objects (no eager programs), for the wave BVH
     (CompiledScene::wobjs; tests/test_gpu_bvh.py):
       grid  576 spheres on a 24 x 24 lattice over a floor (every 5th
             reflective, every 7th refractive), 4 lights;

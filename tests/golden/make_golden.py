@@ -224,7 +224,8 @@ def make_crowd():
 
 
 def make_bvh():
-    """Scenes of more than 64 objects for the wave BVH (scenes.bvh_scenes), both modes."""
+    """Scenes of more than kWaveBvhMin = 256 objects (the wave BVH threshold) for the wave BVH
+    (scenes.bvh_scenes), both modes."""
     data = {}
     for name, scene in scenes.bvh_scenes(dpi=16).items():
         sc = rtamd.load_scene_from_json_text(json.dumps(scene))

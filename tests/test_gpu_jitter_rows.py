@@ -146,7 +146,7 @@ def test_frame_chunks_on_two_streams(gpu, mode):
     assert (st.rays_intersect, st.rays_occluded) == (st1.rays_intersect, st1.rays_occluded)
 
 
-TSEG = 64 * 624   # checkpoint-table segment (rtamd::kTableK twist blocks)
+TSEG = 16 * 624   # checkpoint-table segment: rtamd::kTableK = 16 twist blocks of 624 words (mt_jump.hpp)
 
 
 @pytest.mark.gpu
@@ -158,9 +158,9 @@ TSEG = 64 * 624   # checkpoint-table segment (rtamd::kTableK twist blocks)
     (FRAME_8K - 64, FRAME_8K, FRAME_8K // 2 - 32, 32),       # last pixels of 8K (table of 26.6k checkpoints)
 ])
 def test_jitter_table_path_matches_serial(gpu, q0, q1, first, count):
-    """The frame path (K = 0 in the hook): resident checkpoint table every 64
-    twist blocks + the one-wavefront fill kernel, draw for draw against the
-    serial stream."""
+    """The frame path (K = 0 in the hook): resident checkpoint table every
+    kTableK = 16 twist blocks + the one-wavefront fill kernel, draw for draw
+    against the serial stream; the cases land on and across segment edges."""
     dev = _device_draws(q0, q1, first, count, K=0)
     ref = _oracle_draws(first, count)
     assert np.array_equal(dev, ref)

@@ -41,23 +41,41 @@ def test_dist_partition(rt, H, world, mode, S):
     """rt_dist_rows_mode: interleaved strips of RT_STRIP_ROWS
     (paper mode RT_PAPER_STRIP_ROWS), every output row on exactly one rank,
     ascending per rank, balanced to a strip."""
+    import frame_dist
+
     rows = [rt.dist_rows(H, world, r, mode) for r in range(world)]
     flat = sorted(x for rr in rows for x in rr)
     assert flat == list(range(H))
+    own = frame_dist.strip_owners((H + S - 1) // S, world, mode)
     for r, rr in enumerate(rows):
         assert rr == sorted(rr)
-        assert all((x // S) % world == r for x in rr)
-    sizes = [len(rr) for rr in rows]
-    assert max(sizes) - min(sizes) <= S
+        assert all(own[x // S] == r for x in rr)   # whole strips
+    # the non-root ranks balanced to a strip; the root near its weight
+    n_strips = [sum(1 for o in own if o == r) for r in range(world)]
+    if world > 1:
+        assert max(n_strips[1:]) - min(n_strips[1:]) <= 1
+        w0 = max(500, 1000 - (30 if mode == 1 else 8) * world) / 1000
+        assert abs(n_strips[0] - w0 * (len(own) - n_strips[0]) / (world - 1)) <= 1.5
     if mode == 0:
         assert rows == [rt.dist_rows(H, world, r) for r in range(world)]   # rt_dist_rows = standard
 
 
+def test_strip_owners_rotate_per_round():
+    """Equal weights (RGB8 output): round k of `world` strips starts at rank
+    k mod world, so no rank owns one phase of the world*S-row period."""
+    import frame_dist
+
+    own = frame_dist.strip_owners(64, 8, mode=0, kind=1)
+    for k in range(8):
+        assert own[8 * k:8 * k + 8] == [(k + i) % 8 for i in range(8)]
+
+
 def test_dist_partition_matches_python_mirror(rt):
     import frame_dist
-    for H, world in [(2160, 8), (1081, 3), (7, 2)]:
-        for r in range(world):
-            assert rt.dist_rows(H, world, r) == frame_dist.strip_rows(H, r, world)
+    for H, world in [(2160, 8), (1081, 3), (7, 2), (4320, 8), (4320, 5)]:
+        for mode in (0, 1):
+            for r in range(world):
+                assert rt.dist_rows(H, world, r, mode) == frame_dist.strip_rows(H, r, world, frame_dist.strip_for(mode))
 
 
 def _decode_png(path):

@@ -1,0 +1,10 @@
+# Round-4: light-centred culls, margins fixed: parity subset + bench + instruction mix (config 4).
+set -o pipefail
+export TMPDIR=/tmp
+T=${TAG:-r04g}
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullres_parity.py tests/test_gpu_bvh.py tests/test_gpu_crowd.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo "tests failed"; grep -E "FAIL|Error|assert" gpurun_out/${T}_gpu_tests.log | head -30; tail -30 gpurun_out/${T}_gpu_tests.log; exit 1; }
+tail -2 gpurun_out/${T}_gpu_tests.log
+timeout -k 10 300 python bench.py --steps 200 --no-cpu --no-pmc --no-cli > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { echo bench failed; tail gpurun_out/${T}_bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/${T}_bench.json')); r=d['roofline']; print(d['value'], d['ms_per_step'], r['kernel_ms'], r['frac'], r['executed_frac'], r['occupancy'])"
+timeout -k 10 400 bash tools/gpu/pmc_detail.sh 4 > gpurun_out/${T}_pmc_detail_cfg4.txt 2>&1 || { echo "pmc failed"; tail gpurun_out/${T}_pmc_detail_cfg4.txt; exit 1; }
+grep -E "k_std|SQ_INSTS_VALU  |SQ_INSTS_VALU |SQ_INSTS_SALU|SQ_WAVES" gpurun_out/${T}_pmc_detail_cfg4.txt | head

@@ -169,12 +169,13 @@ def product_ranks(args):
             base = worst
         rows = rtamd.dist_rows(H, N, 0, mode)
         strip = frame_dist.strip_for(mode)
-        a_last, b_last = frame_dist.chunk_bounds(len(rows), 4, strip)[-1]
+        nch = int(os.environ.get("RT_DIST_CHUNKS_PAPER" if mode == 1 else "RT_DIST_CHUNKS", "4"))
+        a_last, b_last = frame_dist.chunk_bounds(len(rows), max(1, min(4, nch)), strip)[-1]
         bpp = 1 if mode == 1 else (3 if args.rgb8 else 24)   # paper: one code byte per pixel
         last_chunk = (b_last - a_last) * W * bpp
         g64 = last_chunk / 64e9 * 1e3 if N > 1 else 0.0
         g153 = last_chunk / 153e9 * 1e3 if N > 1 else 0.0
-        out = {"config": args.config, "world": N, "path": "product rank (rt_test_dist_sim_rank)",
+        out = {"config": args.config, "world": N, "path": "product rank (rt_test_dist_sim_rank)", "chunks": nch,
                "max_rank_wall_ms": round(worst, 3), "rank0_wall_ms": round(per[0]["wall_ms"], 3),
                "min_rank_wall_ms": round(min(p["wall_ms"] for p in per), 3),
                "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
