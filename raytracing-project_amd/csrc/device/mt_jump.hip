@@ -27,6 +27,7 @@
 #include <cstring>
 
 #include "mt_jump.hpp"
+#include "pinned.hpp"
 #include "mt_poly.hpp"
 
 namespace {
@@ -498,7 +499,7 @@ hipError_t mt_launch_fill(const JitterTable& T, const std::vector<JRange>& range
     std::memcpy(job.stage.data() + b_r, segs.data(), b_s);
     job.qmax = ranges.back().qb;
     char* dsc = static_cast<char*>(d_scratch);
-    hipError_t e = hipMemcpyAsync(dsc, job.stage.data(), job.stage.size(), hipMemcpyHostToDevice, stream);
+    hipError_t e = upload_async(job.up, dsc, job.stage.data(), job.stage.size(), stream);
     if (e != hipSuccess) return e;
     FillArgs F{};
     F.K = kTableK;
@@ -630,7 +631,7 @@ hipError_t mt_launch_jitter(const JitterPlan& plan, const std::vector<JRange>& r
     if (b_l) std::memcpy(job.stage.data() + b_r + b_s, lists.data(), b_l);
     job.qmax = qmax;
     char* dsc = static_cast<char*>(d_scratch);
-    hipError_t e = hipMemcpyAsync(dsc, job.stage.data(), job.stage.size(), hipMemcpyHostToDevice, stream);
+    hipError_t e = upload_async(job.up, dsc, job.stage.data(), job.stage.size(), stream);
     if (e != hipSuccess) return e;
     const JRange* dR = reinterpret_cast<const JRange*>(dsc);
     const int64_t* dS = reinterpret_cast<const int64_t*>(dsc + b_r);

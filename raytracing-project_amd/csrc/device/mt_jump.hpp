@@ -62,9 +62,11 @@ __host__ __device__ __forceinline__ double jitter_draw(uint32_t raw0, uint32_t r
 // checkpoints per tree level, ranges) are staged here and uploaded into the
 // caller's device scratch; the host copy stays alive until the stream is
 // synchronised.
+struct PinnedArena;
 struct JitterJob {
     std::vector<char> stage;
     int64_t qmax = 0;
+    PinnedArena* up = nullptr;   // page-locked staging of the job's upload (pinned.hpp), if set
 };
 
 // Only the checkpoints the requested ranges need are computed (the needed

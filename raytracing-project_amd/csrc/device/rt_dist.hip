@@ -977,6 +977,10 @@ extern "C" int rt_test_dist_sim_rank(const rt_scene* s, int W, int H, int mode, 
     static std::map<std::pair<int, int>, std::unique_ptr<rt_dist>> ranks;
     static DevBuf stage, out;
     std::lock_guard<std::mutex> lk(mu);
+    // every simulated rank on the same two extra streams, as a real rank's
+    // process has them (per-rank streams here would outnumber the device's
+    // hardware queues and serialise a rank's two chunk streams on one queue)
+    static rt_dist streams;
     auto& d = ranks[{world, rank}];
     if (!d) {
         d.reset(new rt_dist);
@@ -984,6 +988,16 @@ extern "C" int rt_test_dist_sim_rank(const rt_scene* s, int W, int H, int mode, 
         d->rank = rank;
         d->sim_stage = &stage;
         HIP_TRY(hipGetDevice(&d->device));
+        const int rs = dist_init_streams(streams);
+        if (rs != RT_OK) return rs;
+        d->comm_st = streams.comm_st;
+        d->alt_st = streams.alt_st;
+        for (auto& e : d->ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& e : d->ev_tb) HIP_TRY(hipEventCreate(&e));
+        for (auto& e : d->ev_gs) HIP_TRY(hipEventCreate(&e));
+        for (auto& e : d->ev_ge) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&d->ev_alt, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&d->ev_desc, hipEventDisableTiming));
     }
     void* o = nullptr;
     if (rank == 0) {

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "mt_jump.hpp"
+#include "pinned.hpp"
 #include "mt_poly.hpp"
 #include "rt.h"
 #include "rt_launch.hpp"
@@ -126,6 +127,7 @@ struct Workspace {
     DBuf paper_i, paper_d, paper_aux, fb;
     rtamd::JitterTable jtab;                  // mt19937(12345) checkpoint table (resident)
     rtamd::JitterJob jjob;
+    rtamd::PinnedArena up;                    // page-locked staging of a frame's uploads (pinned.hpp)
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
@@ -161,11 +163,11 @@ DBuf g_fb;
 int g_fb_dev = 0;
 
 template <class T>
-hipError_t upload(DBuf& b, const std::vector<T>& v, hipStream_t st) {
+hipError_t upload(DBuf& b, const std::vector<T>& v, hipStream_t st, rtamd::PinnedArena* up = nullptr) {
     size_t bytes = v.size() * sizeof(T);
     hipError_t e = b.ensure(bytes ? bytes : 16);
     if (e != hipSuccess || !bytes) return e;
-    return hipMemcpyAsync(b.p, v.data(), bytes, hipMemcpyHostToDevice, st);
+    return rtamd::upload_async(up, b.p, v.data(), bytes, st);
 }
 
 }  // namespace
@@ -377,6 +379,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
+    ws.up.reset();   // (the previous frame's uploads completed: its rt_frame_end synchronised)
 
     SceneView& S = f->S;
     S.nodes = fp32 ? ws.nodes_f.p : ws.nodes.p;
@@ -462,7 +465,8 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         const int64_t q1 = ws.jranges.back().qb;
         HIP_TRY(ws.jit.ensure((size_t)n_rows * 16 * W * sizeof(double)));
         HIP_TRY(ws.jscratch.ensure(rtamd::mt_fill_scratch_bytes(ws.jranges)));
-        HIP_TRY(upload(ws.rows, f->rows_jrow, st));
+        HIP_TRY(upload(ws.rows, f->rows_jrow, st, &ws.up));
+        ws.jjob.up = &ws.up;
         const auto t_l = SClock::now();
         HIP_TRY(rtamd::mt_launch_fill(ws.jtab, ws.jranges, ws.jjob, ws.jscratch.p, ws.jit.as<double>(), st));
         {
@@ -510,7 +514,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         // (+ the ext lists of the trace calls: every entry at most once, each
         // run padded by < 8 to a wave boundary: <= 8 * n_ext entries)
         HIP_TRY(ws.paper_aux.ensure((ints.size() + 8 * (size_t)f->n_ext) * sizeof(int32_t)));
-        HIP_TRY(hipMemcpyAsync(ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(rtamd::upload_async(&ws.up, ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), st));
         const size_t npx = (size_t)f->n_ext * W;
         HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
         HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
@@ -628,7 +632,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
             f->list_used += (int)list.size();
             f->stage.push_back(std::move(list));
             const std::vector<int32_t>& L = f->stage.back();
-            HIP_TRY(hipMemcpyAsync(d_list, L.data(), L.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+            HIP_TRY(rtamd::upload_async(&ws.up, d_list, L.data(), L.size() * sizeof(int32_t), st));
             dim3 g1((W + 15) / 16, (P.n_list + 15) / 16);
             if (f->fp32) rtf::launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
             else if (f->big) rtdb::launch_paper(true, true, f->count_ops, g1, st, f->S, P);
@@ -726,6 +730,7 @@ int rtamd::release_device_workspaces() {
                         &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb})
             b->release();
         w->jtab.release();
+        w->up.release();
         for (auto& e : w->ev) {
             if (e) (void)hipEventDestroy(e);
             e = nullptr;
