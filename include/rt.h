@@ -371,8 +371,9 @@ int rt_stream_create(void** stream_out);             /* non-blocking HIP stream 
 int rt_stream_destroy(void* stream);
 /* Page-lock an existing host buffer (hipHostRegister) so that the output
  * copies of rt_render_rgb8 / rt_render_multi into it run as direct DMA
- * instead of through the runtime's pageable staging (the `ray` CLI registers
- * its output buffer while HIP starts).  Unregister before freeing it. */
+ * instead of through the runtime's pageable staging: for callers that render
+ * many frames into the same buffer (registering 25 MB costs ~50 ms, so the
+ * one-frame `ray` CLI does not).  Unregister before freeing it. */
 int rt_host_register(void* host, size_t bytes);
 int rt_host_unregister(void* host);
 /* One-time setup costs of this process so far, host wall clock in ms:

@@ -78,17 +78,14 @@ int main(int argc, char** argv) {
             if (!done) (void)rt_shutdown();
         }
     } teardown;
-    // the output bytes are written by the device path into this buffer; on a
-    // helper thread, while the main thread initialises HIP, its pages are
-    // touched and then page-locked (rt_host_register), so the one D2H copy runs
-    // as direct DMA instead of through the runtime's pageable staging (the
-    // process's first large pageable copy: ~10 ms for 25 MB)
+    // the output bytes are written by the device path into this buffer; its
+    // pages are touched here, on a helper thread, while the main thread
+    // initialises HIP (page faults of a fresh 25 MB buffer otherwise land on
+    // the D2H copy).  Page-locking it as well (rt_host_register) was measured
+    // and rejected: registering 25 MB took 47-54 ms and slowed the concurrent
+    // scene upload and jitter table; the first pageable D2H costs ~8 ms.
     std::vector<uint8_t> rgb;
-    bool registered = false;
-    std::thread prefault([&rgb, &registered, W, H] {
-        rgb.assign((size_t)W * H * 3, 0);
-        registered = rt_host_register(rgb.data(), rgb.size()) == RT_OK;
-    });
+    std::thread prefault([&rgb, W, H] { rgb.assign((size_t)W * H * 3, 0); });
     // HIP runtime initialisation (the first HIP call of the process), timed on its own for --stats
     const auto t_hip0 = std::chrono::steady_clock::now();
     (void)rt_device_count();
@@ -111,7 +108,6 @@ int main(int argc, char** argv) {
         return 4;
     }
     const auto t2 = std::chrono::steady_clock::now();
-    if (registered) (void)rt_host_unregister(rgb.data());
     teardown.done = true;
     (void)rt_shutdown();
     const auto t3 = std::chrono::steady_clock::now();
