@@ -87,6 +87,10 @@ int rt_test_dist_inject(struct rt_dist* d, int what);
  * current device through the product's rank path, the RCCL gather replaced by
  * a device copy (rank 0 also places every slot).  Ranks are cached, so a
  * repeated call times a warm rank.  For per-rank timing (tools/sim_ranks.py). */
+/* CPU: the paper-mode output code decoder of distributed frames
+ * (rtamd::paper_code_value): bits 0-2 edge index in {0, 0.3, 0.5, 0.6, 0.9},
+ * bit 3 halved at the frame border, bit 4 the hatch bit (white). */
+double rt_test_paper_code_value(int code);
 int rt_test_dist_sim_rank(const struct rt_scene* s, int W, int H, int mode, int flags, int world, int rank, int rgb8,
                           struct rt_stats* stats);
 

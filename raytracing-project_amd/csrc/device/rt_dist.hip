@@ -1095,3 +1095,8 @@ extern "C" int rt_test_dist_inject(rt_dist* d, int what) {
     d->inject = what;
     return RT_OK;
 }
+
+// ------------------------------------------------------------- test hook
+// The paper-code decoder the root runs after the gather (host build of the
+// same inline function), for the CPU tests: value of one code byte.
+extern "C" double rt_test_paper_code_value(int code) { return rtamd::paper_code_value((unsigned)code & 31u); }

@@ -113,3 +113,26 @@ def test_unbounded_chunk_and_paper_mode(gpu):
     ref, ost = gpu.oracle_render(sc, sc.width, sc.height, 1, threads=16)
     assert counts == (int(ost.rays_intersect), int(ost.rays_occluded))
     assert np.array_equal(fb, ref)
+
+
+@pytest.mark.gpu
+def test_bvh_counts_every_object_of_every_query(gpu):
+    """Op counting with the BVH: every object of every closest-hit query is
+    either culled (by its own test or its chunk's) or evaluated, so culled +
+    evaluated = queries x objects, with and without the BVH.  (The grid
+    without lights: Scene::occluded stops at its first hit, in an order the
+    BVH changes, so shadow queries have no such invariant.)"""
+    s = scenes.bvh_scenes(16)["grid"]
+    s = dict(s, sources=[])
+    sc = gpu.load_scene_from_json_text(json.dumps(s))
+    n_obj = len(s["objects"])
+    totals = []
+    for flags in (gpu.RT_FLAG_COUNT_OPS, gpu.RT_FLAG_COUNT_OPS | gpu.RT_FLAG_NO_BVH):
+        st = gpu.Stats()
+        gpu.Tracer(sc, sc.width, sc.height, 0, flags=flags).render(st)
+        ops = st.as_dict()["ops"]
+        evaluated = ops["sphere_isect"] + ops["half_isect"]
+        totals.append((ops["culled"] + evaluated, int(st.rays_intersect)))
+    (t_bvh, q_bvh), (t_flat, q_flat) = totals
+    assert q_bvh == q_flat
+    assert t_bvh == t_flat == q_bvh * n_obj

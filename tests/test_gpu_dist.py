@@ -315,3 +315,22 @@ def test_shutdown_releases_and_recovers(gpu):
     gpu.shutdown()   # idempotent
     assert np.array_equal(gpu.Tracer(sc, W, H, mode).render(), a)
     assert np.array_equal(gpu.render_rgb8(sc, W, H, mode, 1), a8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 11])
+@pytest.mark.parametrize("world", [2, 5, 8])
+def test_dist_paper_codes_crowd(gpu, seed, world):
+    """Paper-mode distributed frames carry one output code per pixel
+    (rtamd::paper_code_value) through the gather: seeded 150-object crowd
+    scenes (many materials, depth and normal edges, frame-border halving) on
+    simulated ranks decode bit-exactly to rt_render's frame, in FP64 and RGB8,
+    and every pixel value lies in the paper alphabet."""
+    sc = gpu.load_scene_from_json_text(json.dumps(scenes.crowd_scene(seed, dpi=24)))
+    W, H = sc.width, sc.height
+    want = gpu.Tracer(sc, W, H, 1).render()
+    vals = set(np.unique(want).tolist())
+    assert vals <= {0.0, 0.2, 1.0, 1.0 * (1.0 - (0.45 - 0.3) * 0.4), 1.0 * (1.0 - (0.5 - 0.3) * 0.4)} | {0.0}
+    got = gpu.render_dist_sim(sc, W, H, 1, world)
+    assert np.array_equal(got, want)
+    assert np.array_equal(gpu.render_dist_sim(sc, W, H, 1, world, rgb8=True), gpu.to_rgb8(want))

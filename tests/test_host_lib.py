@@ -191,3 +191,32 @@ def test_runtime_guard_refuses_two_runtimes(rt, monkeypatch):
         rt.check_one_hip_runtime()
     monkeypatch.setattr(rt, "mapped_libraries", lambda stem: [rocm + "/lib/libamdhip64.so.7"])
     assert rt.check_one_hip_runtime().startswith(rocm)
+
+
+def test_paper_code_decoder_matches_reference_expression(rt):
+    """Distributed paper-mode frames gather one code byte per pixel; the root
+    decodes it (rtamd::paper_code_value) into the value tracer.cpp:258-281
+    computes from the edge strength (tracer.cpp:133-178: the max of 0.9 /
+    0.6 / 0.5 / 0.3 or 0, halved when a neighbour is outside the frame) and
+    the hatch bit (tracer.cpp:188-205), bit for bit in FP64."""
+    lib = rt.amd_lib()
+    lib.rt_test_paper_code_value.restype = C.c_double
+    lib.rt_test_paper_code_value.argtypes = [C.c_int]
+    raw = [0.0, 0.3, 0.5, 0.6, 0.9]
+    seen = set()
+    for i, e0 in enumerate(raw):
+        for half in (0, 1):
+            for h in (0, 1):
+                edge = e0 * 0.5 if half else e0
+                if edge > 0.8:
+                    want = 0.0
+                elif edge > 0.5:
+                    want = 0.2
+                else:
+                    want = 1.0 if h else 0.0
+                    if edge > 0.3:
+                        want *= (1.0 - (edge - 0.3) * 0.4)
+                got = lib.rt_test_paper_code_value(i | (8 if half else 0) | (16 if h else 0))
+                assert struct.pack("<d", got) == struct.pack("<d", want), (i, half, h, got, want)
+                seen.add(got)
+    assert {0.0, 0.2, 1.0} <= seen and len(seen) >= 5   # incl. the darkened whites of edges 0.45 / 0.6*0.5...
