@@ -1937,6 +1937,86 @@ __device__ __forceinline__ bool ball_cone(const float4 g, const LightCone& K, fl
     return lrec_ball_cone(make_float4(wx, wy, wz, w2), g.w, magw, K);
 }
 
+// Sub-bundles of a shadow query (the wave BVH kernels).  Where a tile
+// straddles depth edges of an incoherent scene its hull is wide and lets
+// dozens of objects through that no segment reaches (a pixel's 8 samples do
+// not help: one straddling pixel is as wide as the tile).  So the querying
+// lanes are clustered greedily by their ray origins: the first remaining lane
+// q and every remaining lane within tau = 1/64 of q's distance to the light
+// form a cluster of radius rho_c <= tau, at most kMaxClusters of them (the
+// last takes every lane left).  A cluster's segments start within rho_c of
+// q_c (plus eps along the ray) and end within 2 eps of L, so they lie within
+// 2 emax of the cone from L over B(q_c, rho_c + emax).  Every lane forms its
+// own cluster's cone; lane j tests its record (c0, c1) against each cluster's
+// cone (read from the cluster's first lane) and the ballot of "any cluster
+// reaches it" refines the wave's candidate mask.  Conservative like the wave
+// hull; a cluster whose cone is not valid keeps every object.  Every lane
+// must be active.
+#ifndef RT_SUB_MIN
+#define RT_SUB_MIN 1
+#endif
+constexpr int kSubBundleMin = RT_SUB_MIN;   // candidates before the refinement runs (A/B: RT_SUB_MIN)
+#ifndef RT_MAXCL
+#define RT_MAXCL 6
+#endif
+constexpr int kMaxClusters = RT_MAXCL;
+__device__ __forceinline__ uint64_t sub_bundle_mask(const float4 c0, const float4 c1, const DRay& r0, real tmin,
+                                                    bool need, uint64_t nm, float Lx, float Ly, float Lz) {
+    const int lane = __lane_id();
+    const float ox = (float)r0.o.x, oy = (float)r0.o.y, oz = (float)r0.o.z;
+    const bool bad = need && !__builtin_isfinite(ox + oy + oz);
+    if (__any(bad)) return ~0ull;
+    const float e = need ? (float)tmin : 0.0f;
+    const float emax = __uint_as_float(wave_max_u32(__float_as_uint(e))) * 1.000001f;
+    // greedy clusters: each lane ends with its cluster's centre and radius^2
+    float cx = ox, cy = oy, cz = oz, cr2 = 0.0f;
+    uint64_t rem = nm, leaders = 0;
+    for (int k = 0; rem && k < kMaxClusters; ++k) {
+        const int f = __builtin_ctzll(rem);
+        leaders |= 1ull << f;
+        const float qx = rdlane_f(ox, f), qy = rdlane_f(oy, f), qz = rdlane_f(oz, f);
+        const float lx = qx - Lx, ly = qy - Ly, lz = qz - Lz;
+        const float tau2 = (k + 1 == kMaxClusters) ? __builtin_inff()
+                                                   : 2.4414e-4f * __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
+        const float dx = ox - qx, dy = oy - qy, dz = oz - qz;
+        const float d2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+        const bool in = ((rem >> lane) & 1ull) && d2 <= tau2;
+        const uint64_t mb = __ballot(in);
+        const float r2 = __uint_as_float(wave_max_u32(__float_as_uint(in ? d2 : 0.0f)));
+        if (in) {
+            cx = qx, cy = qy, cz = qz;
+            cr2 = r2;
+        }
+        rem &= ~mb;
+    }
+    // the lane's cluster's cone
+    const float ux = cx - Lx, uy = cy - Ly, uz = cz - Lz;
+    const float dq = sqrt_cull(__builtin_fmaf(ux, ux, __builtin_fmaf(uy, uy, uz * uz)));
+    const float mq = __builtin_fabsf(cx) + __builtin_fabsf(cy) + __builtin_fabsf(cz) + __builtin_fabsf(Lx) +
+                     __builtin_fabsf(Ly) + __builtin_fabsf(Lz);
+    const float rho = __builtin_fmaf(sqrt_cull(cr2) + emax, 1.00001f, 1e-6f * (mq + 1.0f));
+    const float inv = __builtin_amdgcn_rcpf(dq);
+    const float sb = __builtin_fminf(1.0f, rho * inv * 1.00001f + 1e-6f);
+    const float cb = sqrt_cull(__builtin_fmaxf(0.0f, __builtin_fmaf(-sb, sb, 1.0f))) * 0.99999f - 1e-6f;
+    const bool ok = (dq > rho * 1.0001f) && (cb > 0.0f) && __builtin_isfinite(rho);
+    const float gv[14] = {ux * inv, uy * inv, uz * inv, cb, sb, dq * 0.99999f, (dq + rho) * 1.00001f,
+                          rho * __builtin_amdgcn_rcpf(cb) * 1.00001f + 1e-6f * mq, rho, 2.0f * emax, cx, cy, cz, mq};
+    bool pass = false;
+    while (leaders) {
+        const int lg = __builtin_ctzll(leaders);
+        leaders &= leaders - 1;
+        if (!__builtin_amdgcn_readlane(ok ? 1 : 0, lg)) return ~0ull;   // keep every object
+        LightCone K;
+        K.ax = rdlane_f(gv[0], lg), K.ay = rdlane_f(gv[1], lg), K.az = rdlane_f(gv[2], lg);
+        K.cb = rdlane_f(gv[3], lg), K.sb = rdlane_f(gv[4], lg), K.dq = rdlane_f(gv[5], lg);
+        K.xe = rdlane_f(gv[6], lg), K.rend = rdlane_f(gv[7], lg), K.rho = rdlane_f(gv[8], lg);
+        K.emax = rdlane_f(gv[9], lg), K.qx = rdlane_f(gv[10], lg), K.qy = rdlane_f(gv[11], lg);
+        K.qz = rdlane_f(gv[12], lg), K.mq = rdlane_f(gv[13], lg);
+        pass = pass || lrec_touch(c0, c1, K);
+    }
+    return __ballot(pass);
+}
+
 // Scene::occluded (scene.cpp:33-42) for the querying lanes of a fully active
 // wave, light li of S.lights.  Returns false for lanes with need = false.
 //
@@ -2008,6 +2088,14 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
                 const int ktype = __float_as_int(k1.x);
                 const bool pass = (c < nch) & ((ktype != 2) | ball_cone(k0, K, Lx, Ly, Lz));
                 cm = (cone && exec_full()) ? __ballot(pass) : ~0ull;
+                if (cone && __builtin_popcountll(cm) > kSubBundleMin && exec_full()) {
+                    // the chunk balls against the per-pixel hulls (light-relative on the fly)
+                    const float wx = k0.x - Lx, wy = k0.y - Ly, wz = k0.z - Lz;
+                    const float4 q0 = make_float4(wx, wy, wz, __builtin_fmaf(wx, wx, __builtin_fmaf(wy, wy, wz * wz)));
+                    const float4 q1 = make_float4(k1.x, k0.w, __builtin_fabsf(wx) + __builtin_fabsf(wy) + __builtin_fabsf(wz) + k0.w,
+                                                  0.0f);
+                    cm &= sub_bundle_mask(q0, q1, r0, tmin, need, nm, Lx, Ly, Lz);
+                }
             }
             if (!((cm >> (ch & 63)) & 1ull)) {
                 if constexpr (!std::is_same<CT, Cnt<false>>::value)
@@ -2027,6 +2115,12 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
         uint64_t m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        // Sub-bundles: where the wave's hull lets many objects of a chunk
+        // through (a tile straddling depth edges of an incoherent scene), each
+        // object is tested again against the eight per-pixel hulls (a pixel's
+        // 8 samples hit close together) and kept if any of them reaches it.
+        if (cone && __builtin_popcountll(m) > kSubBundleMin && exec_full())
+            m &= sub_bundle_mask(c0, c1, r0, tmin, need, nm, Lx, Ly, Lz);
         cnt.pe(PH_WAVE_SETUP);
 #if defined(RT_ABL) && RT_ABL == 2   // diagnostic: setup + transposed test only
         if (m != 12345) return false;

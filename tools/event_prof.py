@@ -22,8 +22,13 @@ EVENTS = ["shadow_queries", "shadow_candidates", "shadow_object_hits", "shadow_c
 
 
 def main():
-    cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    text, mode = scenes.config_json(cfg)
+    arg = sys.argv[1] if len(sys.argv) > 1 else "4"
+    if arg.startswith("bvh"):   # e.g. bvh4096: tools/bvh_perf.py's random-sphere scene
+        import json
+        cfg, text, mode = arg, json.dumps(scenes.bvh_perf_scene(int(arg[3:]), dpi=480)), 0
+    else:
+        cfg = int(arg)
+        text, mode = scenes.config_json(cfg)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
     buf = rtamd.DeviceBuffer(H * W * 3 * 8)
