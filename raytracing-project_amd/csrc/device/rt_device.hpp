@@ -2685,25 +2685,41 @@ struct Frame {
 // leave only the lanes still bouncing active and every query would fall back
 // to testing all objects).  Each lane's arithmetic is the one of trace()
 // below, step for step.
+//
+// A step's children (the reflected and refracted rays, tracer.cpp:38-68) are
+// formed and pushed BEFORE the step is shaded: they depend only on the hit,
+// and after shade() the step then needs nothing but its direct colour and
+// the stack (the next ray is read back from the frame).  So the ray, the hit
+// point and the normal are dead across shade(), whose shadow queries set the
+// kernel's register peak; kept live there they cost ~320 B/lane of spill slots
+// and 32 % on a frame without bounces.
 template <bool EAGER, bool DEEP, bool DL, int WV, class CT>
-__device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+__device__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     Frame stk[kMaxDepth];
+    // The ray each step traces lives in memory, not registers: slot k < sp is
+    // the next ray of frame k (its reflected child, later its refracted one),
+    // slot kMaxDepth the camera ray.  A step loads it, and it is dead by the
+    // time the step is shaded (a loop-carried register copy stayed live
+    // across shade() on every path).
+    DRay nxt[kMaxDepth + 1];
+    nxt[kMaxDepth] = r0;
+    int rsel = kMaxDepth;
     int sp = 0;
     int depth = 0;
     const int limit = S.rec_limit;
-    V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));
+    stk[0].total = v3(RV(0.0), RV(0.0), RV(0.0));   // (a finished path's colour is parked in stk[0].total)
     bool alive = true;
     const bool wave_ok = __builtin_amdgcn_read_exec() == ~0ull;
     bool first_step = true;
     while (__any(alive)) {
         // ---- evaluate node (r, depth) on the lanes still tracing
+        const DRay r = nxt[rsel];
         const bool eval = alive && depth < limit;
         if (!first_step) {
             cnt.ev(EV_BOUNCE);
             cnt.evn(EV_COMPACT_LEAF, (unsigned)__builtin_popcountll(__ballot(eval)));
         }
         first_step = false;
-        if (alive && !eval) ret = v3(RV(0.0), RV(0.0), RV(0.0));
         real ht = RV(0.0);
         DHit h;
         h.p = h.n = v3(RV(0.0), RV(0.0), RV(0.0));
@@ -2714,63 +2730,67 @@ __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t&
         const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2)>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
         cnt.pe(PH_PRIMARY);
         const bool sh = eval && hit;
-        if (eval && !hit) ret = v3(S.bg[0], S.bg[1], S.bg[2]);
-        V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
-        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, sh);
+        // ---- the step's children, pushed before shading (tracer.cpp:38-68)
         bool descend = false;
-        if (sh) {
-            if (h.mat < 0) {
-                ret = direct;
-            } else {
-                const MatT* mat = &S.mats[h.mat];
-                const bool can = depth < limit - 1;
-                const bool want_refl = mat->kr > RV(0.0) && can;
-                bool want_refr = false;
-                DRay refr;
-                if (mat->kt > RV(0.0) && can) {
-                    const real eta = h.ff ? (S.medium_index / mat->refractive_index)
-                                          : (mat->refractive_index / S.medium_index);
+        if (sh && h.mat >= 0) {
+            const MatT* mat = &S.mats[h.mat];
+            const bool can = depth < limit - 1;
+            const bool want_refl = mat->kr > RV(0.0) && can;
+            bool want_refr = false;
+            DRay refr;
+            if (mat->kt > RV(0.0) && can) {
+                const real eta = h.ff ? (S.medium_index / mat->refractive_index)
+                                      : (mat->refractive_index / S.medium_index);
+                const V3 inc = normalized(r.d);
+                const real cos_i = -dot3(inc, h.n);   // tracer.cpp:100-104
+                const real st2 = eta * eta * dmax(RV(0.0), RV(1.0) - cos_i * cos_i);
+                if (!(st2 >= RV(1.0))) {
+                    want_refr = true;
+                    const real cos_t = sqrt_r(RV(1.0) - st2);   // tracer.cpp:87-98
+                    const real k = eta * cos_i - cos_t;
+                    const V3 rd = normalized(v3(inc.x * eta + h.n.x * k, inc.y * eta + h.n.y * k,
+                                                inc.z * eta + h.n.z * k));
+                    const V3 ro = h.ff ? v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6))
+                                       : v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6));
+                    refr = make_ray(ro, rd);
+                }
+            }
+            if (want_refl || want_refr) {
+                Frame& fr = stk[sp];
+                fr.mat = h.mat;
+                fr.want_refr = want_refr;
+                fr.refr = refr;
+                cnt.inc(RT_OPC_SECONDARY);
+                if (want_refl) {
                     const V3 inc = normalized(r.d);
-                    const real cos_i = -dot3(inc, h.n);   // tracer.cpp:100-104
-                    const real st2 = eta * eta * dmax(RV(0.0), RV(1.0) - cos_i * cos_i);
-                    if (!(st2 >= RV(1.0))) {
-                        want_refr = true;
-                        const real cos_t = sqrt_r(RV(1.0) - st2);   // tracer.cpp:87-98
-                        const real k = eta * cos_i - cos_t;
-                        const V3 rd = normalized(v3(inc.x * eta + h.n.x * k, inc.y * eta + h.n.y * k,
-                                                    inc.z * eta + h.n.z * k));
-                        const V3 ro = h.ff ? v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6))
-                                           : v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6));
-                        refr = make_ray(ro, rd);
-                    }
-                }
-                if (want_refl || want_refr) {
-                    Frame fr;
-                    fr.total = direct;
-                    fr.mat = h.mat;
-                    fr.want_refr = want_refr;
-                    fr.refr = refr;
-                    if (want_refl) {
-                        cnt.inc(RT_OPC_SECONDARY);
-                        const V3 inc = normalized(r.d);
-                        const real k = RV(2.0) * dot3(inc, h.n);   // reflect (tracer.cpp:76-78)
-                        const V3 rd = normalized(v3(inc.x - h.n.x * k, inc.y - h.n.y * k, inc.z - h.n.z * k));
-                        const V3 ro = h.ff ? v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6))
-                                           : v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6));
-                        fr.stage = 0;
-                        stk[sp++] = fr;
-                        r = make_ray(ro, rd);
-                    } else {
-                        cnt.inc(RT_OPC_SECONDARY);
-                        fr.stage = 1;
-                        stk[sp++] = fr;
-                        r = refr;
-                    }
-                    depth = sp;
-                    descend = true;
+                    const real k = RV(2.0) * dot3(inc, h.n);   // reflect (tracer.cpp:76-78)
+                    const V3 rd = normalized(v3(inc.x - h.n.x * k, inc.y - h.n.y * k, inc.z - h.n.z * k));
+                    const V3 ro = h.ff ? v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6))
+                                       : v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6));
+                    fr.stage = 0;
+                    nxt[sp] = make_ray(ro, rd);
                 } else {
-                    ret = direct;
+                    fr.stage = 1;
+                    nxt[sp] = refr;
                 }
+                ++sp;
+                descend = true;
+            }
+        }
+        const V3 wo = normalized(vneg(r.d));
+        V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
+        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV>(S, ht, h, wo, n_occl, cnt, sh);
+        // the step's value (a finished lane's colour is in memory, so nothing
+        // but the stack state is carried across steps)
+        V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));
+        if (eval && !hit) ret = v3(S.bg[0], S.bg[1], S.bg[2]);
+        if (sh) {
+            if (descend) {
+                stk[sp - 1].total = direct;
+                rsel = sp - 1;
+                depth = sp;
+            } else {
+                ret = direct;
             }
         }
         if (alive && !descend) {
@@ -2784,7 +2804,8 @@ __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t&
                     if (fr.want_refr) {
                         cnt.inc(RT_OPC_SECONDARY);
                         fr.stage = 1;
-                        r = fr.refr;
+                        nxt[sp - 1] = fr.refr;
+                        rsel = sp - 1;
                         depth = sp;
                         resumed = true;
                         break;
@@ -2797,10 +2818,13 @@ __device__ V3 trace_wave(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t&
                     --sp;
                 }
             }
-            if (!resumed) alive = false;
+            if (!resumed) {
+                alive = false;
+                stk[0].total = ret;   // (sp == 0: the stack is free)
+            }
         }
     }
-    return ret;
+    return stk[0].total;
 }
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
