@@ -251,6 +251,10 @@ __device__ __forceinline__ real crosshatch(real lum, int x, int y) {
     return draw ? RV(0.0) : RV(1.0);
 }
 
+// CODES: a distributed frame's rank writes paper_code bytes (P.code) instead
+// of FP64 pixels (separate instance, so the one-GPU kernel carries none of
+// the code bookkeeping).
+template <bool CODES>
 __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     }
     if (valid < 4) maxEdge *= RV(0.5);
     const real edge = maxEdge;
-    if (P.code) {
+    if constexpr (CODES) {
         // distributed frames: the pixel's place in the output alphabet
         // (rtamd::paper_code), decoded bit-exactly on the root after the gather
         const bool h = edge <= RV(0.5) && crosshatch(P.lum[ci], x, y) != RV(0.0);
@@ -474,7 +478,8 @@ const void* paper_kernel(bool e, bool d, bool wv, bool bv) {
 }
 
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {
-    hipLaunchKernelGGL(k_paper_finish, grid, dim3(256), 0, st, P);
+    if (P.code) hipLaunchKernelGGL(k_paper_finish<true>, grid, dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(k_paper_finish<false>, grid, dim3(256), 0, st, P);
 }
 
 }  // namespace RT_NS
