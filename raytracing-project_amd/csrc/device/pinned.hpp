@@ -14,7 +14,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -63,6 +65,23 @@ inline hipError_t upload_async(PinnedArena* a, void* dst, const void* src, size_
     if (!n) return hipSuccess;
     const void* s = a ? a->put(src, n) : nullptr;
     return hipMemcpyAsync(dst, s ? s : src, n, hipMemcpyHostToDevice, st);
+}
+
+// Wait for an event by polling it (yielding the core between polls; after
+// ~20 ms, 50 us sleeps).  A blocking wait - the pageable counter copy
+// rt_frame_end used to make - resumed the host ~115 us after the GPU had
+// finished (profiles/r04t_api_timeline.txt): 1-2 % of an 8 ms frame, 10 % of
+// a 1 ms rank share.
+inline hipError_t spin_wait(hipEvent_t ev) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return q;
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20))
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
 }
 
 }  // namespace rtamd

@@ -169,6 +169,14 @@ __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_
     std_body<false, false, true, C, false, WV>(S, P);   // (no directional lights: those scenes take D)
 }
 
+// A primary wave's (start, end) tick slot: group-major, 2 * gridDim.x waves
+// (8-column tiles) per 8-entry list group.
+__device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
+    const unsigned w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const unsigned g = blockIdx.y * 2 + (w >> 1), xt = blockIdx.x * 2 + (w & 1);
+    return P.gtime + 2 * ((size_t)g * (2 * gridDim.x) + xt);
+}
+
 template <bool E, bool D, bool C, bool DL = true, int WV = 0>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
@@ -179,6 +187,11 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     // (list entries < 0 pad a run of consecutive rows to a wave boundary)
     const int ei = li < P.n_list ? P.ext_list[li] : -1;
     const bool active = x < P.W && ei >= 0;
+    // the wave's cost for the next frame's launch order (rt_render.hip
+    // order_paper_groups): its start and end wall-clock ticks, stored into
+    // its own slot (nothing held across the kernel; one-address atomics per
+    // list group serialised the waves: +18 % frame time)
+    if (P.gtime && __lane_id() == 0) paper_wave_slot(P)[0] = (unsigned)wall_clock64();
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
     cnt.init();
@@ -221,6 +234,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         }
     }
     flush_counters(P.counters, ni, no, cnt);
+    if (P.gtime && __lane_id() == 0) paper_wave_slot(P)[1] = (unsigned)wall_clock64();
 }
 
 template <bool E, bool D, bool C>

@@ -63,6 +63,36 @@ __global__ void k_to_rgb8(const double* __restrict__ fb, size_t n, uint8_t* __re
     }
 }
 
+// The frame's op counters: kCounterSlots x kCounterWords partial sums reduced
+// on the device and stored straight into page-locked host memory, so that
+// rt_frame_end reads 144 B after one event instead of copying 72 KiB through
+// the runtime's pageable staging (which waited ~115 us after the last kernel
+// before the copy even started: profiles/r04t_api_timeline.txt).
+__global__ void __launch_bounds__(64) k_reduce_counters(const unsigned long long* __restrict__ slots,
+                                                        unsigned long long* __restrict__ out,
+                                                        const unsigned int* __restrict__ gtime, int wpg) {
+    // block k < kCounterWords sums word k over the slots (8 independent loads
+    // per lane); block kCounterWords + g sums paper-mode list group g's wave
+    // times (end - start, mod 2^32) over its wpg waves
+    const int k = blockIdx.x, lane = threadIdx.x;
+    if (k >= rtamd::kCounterWords) {
+        const size_t g = k - rtamd::kCounterWords;
+        unsigned v = 0;
+        for (int xt = lane; xt < wpg; xt += 64) {
+            const unsigned* t = gtime + 2 * (g * wpg + xt);
+            v += t[1] - t[0];
+        }
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) reinterpret_cast<unsigned int*>(out + rtamd::kCounterWords)[g] = v;
+        return;
+    }
+    unsigned long long v = 0;
+#pragma unroll
+    for (int sl = lane; sl < rtamd::kCounterSlots; sl += 64) v += slots[(size_t)sl * rtamd::kCounterWords + k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) out[k] = v;
+}
+
 // ------------------------------------------------------------ host side
 #define HIP_TRY(expr)                                                                            \
     do {                                                                                         \
@@ -128,6 +158,14 @@ struct Workspace {
     rtamd::JitterTable jtab;                  // mt19937(12345) checkpoint table (resident)
     rtamd::JitterJob jjob;
     rtamd::PinnedArena up;                    // page-locked staging of a frame's uploads (pinned.hpp)
+    DBuf gtime;                               // paper mode: primary waves' (start, end) ticks (paper_wave_slot)
+    unsigned long long* ctr_host = nullptr;   // page-locked: the frame's reduced counters (k_reduce_counters)
+    size_t ctr_host_words = 0;                //   + the paper-mode list-group costs behind them
+    // paper mode: measured primary-pass cost of each 8-entry list group of a
+    // frame, by the group's first ext index, per frame key (scene, size,
+    // mode, flags, rows): the next frame of that key launches its groups
+    // costliest first (order_paper_groups)
+    std::map<uint64_t, std::vector<uint32_t>> paper_cost;
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
@@ -194,7 +232,9 @@ struct rt_frame {
     std::vector<int32_t> ext_pos;              // output row -> ext index (-1: none)
     std::vector<int> ext_done;                 // primary hit launched by trace call (value - 1); 0 = not yet
     std::vector<hipStream_t> call_st;          // stream of each trace call
-    int list_used = 0;                         // ext-list entries consumed in the aux buffer
+    int list_used = 0;                         // ext-list entries consumed in the aux buffer (a multiple of 16)
+    uint64_t key = 0;                          // paper mode: Workspace::paper_cost key
+    std::vector<std::pair<int, int>> calls;    // paper mode: (list offset, f->stage index) of each launched list
     int n_tev = 0;                             // trace events recorded (ws.tev[0 .. n_tev))
     hipStream_t last_st = nullptr;             // stream of the previous trace call
     std::vector<std::vector<int32_t>> stage;   // host sources of async uploads
@@ -252,6 +292,64 @@ void make_float_scene(SceneCache& f) {
         f.fold_f[i].pc = f.cs.fold[i].pc;
         f.fold_f[i].pad = 0;
     }
+}
+
+// Paper mode launch order.  A wave of k_paper_primary covers one 8-entry
+// group of the ext list; a group's cost varies ~10x over a frame (sky rows
+// against crowded ones, profiles/r04s_strips5.json).  Launched in row order,
+// the costly rows of the lower frame start last and their waves form the
+// launch's tail: one launch of a rank's rows of an 8-way config-5 frame took
+// 0.858 ms in row order, 0.799 ms costliest strips first, 0.994 ms cheapest
+// first (profiles/r04y_order5.jsonl).  So every primary wave stores its
+// start and end ticks (PaperParams::gtime), rt_frame_end sums them per group
+// and keeps them per frame key, and the next frame of that key launches its
+// 16-entry blocks (workgroup rows) costliest first.  Measured: one GPU
+// 5.37 -> 5.33 ms, the slowest of 8 ranks' trace 0.95 -> 0.93 ms
+// (profiles/r04_ab/ab_order.jsonl).  Groups keep their entries (each wave
+// stays on 8 consecutive rows of one strip); only the launch order changes,
+// which no pixel depends on.  A frame with no history runs in row order.
+// primary waves per 8-entry list group (k_paper_primary: 16-column blocks of 2x2 waves)
+int paper_waves_per_group(int W) { return 2 * ((W + 15) / 16); }
+
+uint64_t paper_frame_key(uint64_t uid, int W, int H, int mode, int flags, const int32_t* rows, int n_rows) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](uint64_t v) {
+        for (int i = 0; i < 8; ++i) {
+            h ^= (v >> (8 * i)) & 0xff;
+            h *= 1099511628211ull;
+        }
+    };
+    mix(uid);
+    mix((uint64_t)(uint32_t)W << 32 | (uint32_t)H);
+    mix((uint64_t)(uint32_t)mode << 32 | (uint32_t)flags);
+    mix((uint64_t)n_rows);
+    for (int i = 0; i < n_rows; ++i) mix((uint64_t)(uint32_t)rows[i]);
+    return h;
+}
+
+// Reorders the 16-entry blocks of list (one workgroup row: its four waves
+// share the workgroup's culls, so a block stays one piece) costliest first
+// when every 8-entry group with an entry has a measured cost (else leaves the
+// row order); padding blocks go last.
+void order_paper_groups(std::vector<int32_t>& list, const std::vector<uint32_t>* cost) {
+    if (!cost) return;
+    const size_t nb = list.size() / 16;
+    std::vector<std::pair<uint64_t, size_t>> key(nb);
+    for (size_t b = 0; b < nb; ++b) {
+        uint64_t c = 0;
+        for (size_t g = 2 * b; g < 2 * b + 2; ++g) {
+            int32_t e = -1;
+            for (size_t i = 0; i < 8 && e < 0; ++i) e = list[8 * g + i];
+            if (e < 0) continue;
+            if ((size_t)e >= cost->size() || (*cost)[e] == 0) return;   // not measured: row order
+            c += (*cost)[e];
+        }
+        key[b] = {c, b};
+    }
+    std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    std::vector<int32_t> out(list.size());
+    for (size_t j = 0; j < nb; ++j) std::copy_n(list.begin() + 16 * key[j].second, 16, out.begin() + 16 * j);
+    list.swap(out);
 }
 
 int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int32_t* rows_host, int n_rows,
@@ -511,9 +609,13 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         ints.insert(ints.end(), ext_shade.begin(), ext_shade.end());
         ints.insert(ints.end(), nbr.begin(), nbr.end());
         ints.insert(ints.end(), f->rows.begin(), f->rows.end());
-        // (+ the ext lists of the trace calls: every entry at most once, each
-        // run padded by < 8 to a wave boundary: <= 8 * n_ext entries)
-        HIP_TRY(ws.paper_aux.ensure((ints.size() + 8 * (size_t)f->n_ext) * sizeof(int32_t)));
+        // (+ the ext lists of the trace calls: every entry once, each run padded
+        // by < 8 to a group boundary and each call's list by < 16 to a block)
+        HIP_TRY(ws.paper_aux.ensure((ints.size() + 24 * (size_t)f->n_ext) * sizeof(int32_t)));
+        f->key = paper_frame_key(rtamd::scene_uid(s), W, H, mode, flags, rows_host, n_rows);
+        // primary waves' (start, end) ticks: <= 3 list groups per ext row (the
+        // list capacity / 8), 2 * ceil(W / 16) waves per group
+        HIP_TRY(ws.gtime.ensure((size_t)3 * f->n_ext * paper_waves_per_group(W) * 2 * sizeof(unsigned)));
         HIP_TRY(rtamd::upload_async(&ws.up, ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), st));
         const size_t npx = (size_t)f->n_ext * W;
         HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
@@ -623,12 +725,25 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
         P.lum = dd + 4 * npx;
         P.fb = fb;
         P.code = codes;
+        P.gtime = nullptr;
         P.counters = ctr;
         if (!list.empty()) {
-            if ((size_t)f->list_used + list.size() > 8 * (size_t)n_ext) {
+            while (list.size() % 16) list.push_back(-1);   // whole blocks: the group index is li / 8
+            if ((size_t)f->list_used + list.size() > 24 * (size_t)n_ext) {
                 rtamd::set_last_error("rt_frame_trace: paper-mode list overflow");
                 return RT_ERR_PROCESSING;
             }
+            // RT_PAPER_ORDER (measurement A/B): 0 = row order, untimed; 1 = row
+            // order, timed; 2 (default) = costliest blocks first
+            static const int order_mode = [] { const char* e = std::getenv("RT_PAPER_ORDER"); return e && *e ? std::atoi(e) : 2; }();
+            if (order_mode >= 2) {
+                const auto it = ws.paper_cost.find(f->key);
+                order_paper_groups(list, it == ws.paper_cost.end() ? nullptr : &it->second);
+            }
+            P.n_list = (int)list.size();
+            if (order_mode >= 1)
+                P.gtime = ws.gtime.as<unsigned>() + (size_t)(f->list_used / 8) * paper_waves_per_group(W) * 2;
+            f->calls.emplace_back(f->list_used, (int)f->stage.size());
             f->list_used += (int)list.size();
             f->stage.push_back(std::move(list));
             const std::vector<int32_t>& L = f->stage.back();
@@ -667,15 +782,49 @@ int frame_end(rt_frame* f, rt_stats* stats) {
     std::unique_ptr<rt_frame> own(f);
     Workspace& ws = *f->ws;
     const hipStream_t st = f->st;
-    for (int i = 0; i < f->n_tev; ++i) HIP_TRY(hipStreamWaitEvent(st, ws.tev[i], 0));   // join trace streams
+    // join the other trace streams: one wait on each one's last call (stream
+    // order covers its earlier ones; every wait is a barrier packet on st)
+    for (int i = 0; i < f->n_tev; ++i) {
+        if (f->call_st[i] == st) continue;
+        bool last = true;
+        for (int j = i + 1; j < f->n_tev; ++j) last = last && f->call_st[j] != f->call_st[i];
+        if (last) HIP_TRY(hipStreamWaitEvent(st, ws.tev[i], 0));
+    }
     HIP_TRY(hipEventRecord(ws.ev[2], st));
-    const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
-    std::vector<unsigned long long> slots((size_t)kCounterSlots * kCounterWords);
-    HIP_TRY(hipMemcpyAsync(slots.data(), ws.counters.p, ctr_bytes, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    unsigned long long hc[kCounterWords] = {};
-    for (int sl = 0; sl < kCounterSlots; ++sl)
-        for (int k = 0; k < kCounterWords; ++k) hc[k] += slots[(size_t)sl * kCounterWords + k];
+    const int n_groups = f->list_used / 8;
+    const size_t host_words = kCounterWords + ((size_t)n_groups + 1) / 2;
+    if (!ws.ctr_host || ws.ctr_host_words < host_words) {
+        if (ws.ctr_host) (void)hipHostFree(ws.ctr_host);   // (the previous frame's readback is done)
+        ws.ctr_host = nullptr;
+        ws.ctr_host_words = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ws.ctr_host), host_words * sizeof(unsigned long long),
+                              hipHostMallocDefault));
+        ws.ctr_host_words = host_words;
+    }
+    const unsigned long long* ctr = ws.counters.as<unsigned long long>();
+    const bool timed = f->mode == RT_MODE_PAPER && !f->calls.empty() && ws.gtime.p;
+    hipLaunchKernelGGL(k_reduce_counters, dim3(kCounterWords + (timed ? n_groups : 0)), dim3(64), 0, st, ctr, ws.ctr_host,
+                       ws.gtime.as<unsigned>(), paper_waves_per_group(f->W));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ws.ev[3], st));
+    HIP_TRY(rtamd::spin_wait(ws.ev[3]));
+    unsigned long long hc[kCounterWords];
+    for (int k = 0; k < kCounterWords; ++k) hc[k] = ((volatile unsigned long long*)ws.ctr_host)[k];
+    if (timed) {
+        // this frame's group costs, by each group's first ext index
+        if (ws.paper_cost.size() >= 64 && !ws.paper_cost.count(f->key)) ws.paper_cost.clear();
+        std::vector<uint32_t>& cost = ws.paper_cost[f->key];
+        cost.resize(f->n_ext, 0);
+        const volatile unsigned int* gc = reinterpret_cast<const volatile unsigned int*>(ws.ctr_host + kCounterWords);
+        for (const auto& c : f->calls) {
+            const std::vector<int32_t>& L = f->stage[c.second];
+            for (size_t g = 0; g < L.size() / 8; ++g) {
+                int32_t e = -1;
+                for (size_t i = 0; i < 8 && e < 0; ++i) e = L[8 * g + i];
+                if (e >= 0) cost[e] = std::max(1u, (unsigned)gc[c.first / 8 + g]);
+            }
+        }
+    }
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
         stats->rays_intersect = f->mode == RT_MODE_PAPER ? f->logical_isect : hc[0];
@@ -727,10 +876,14 @@ int rtamd::release_device_workspaces() {
                         &w->lwrec, &w->lgb, &w->fold,
                         &w->wobjs, &w->wctab, &w->worig, &w->wchunk,
                         &w->nodes_f, &w->mats_f, &w->lights_f, &w->dlights_f, &w->fold_f, &w->rows, &w->jit, &w->ckpt,
-                        &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb})
+                        &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb, &w->gtime})
             b->release();
         w->jtab.release();
         w->up.release();
+        if (w->ctr_host) (void)hipHostFree(w->ctr_host);
+        w->ctr_host = nullptr;
+        w->ctr_host_words = 0;
+        w->paper_cost.clear();
         for (auto& e : w->ev) {
             if (e) (void)hipEventDestroy(e);
             e = nullptr;

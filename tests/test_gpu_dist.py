@@ -114,6 +114,24 @@ def test_dist_path_simulated_ranks(gpu, world, name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg5_paper", "snorlax_paper"])
+def test_paper_launch_order_does_not_change_pixels(gpu, name):
+    """Paper frames after the first launch their primary blocks costliest
+    first, from the previous frame's measured wave times (rt_render.hip
+    order_paper_groups): the cold frame (row order) and the reordered frames
+    after it, one-GPU and per simulated rank, are bit-identical."""
+    sc, mode = _scene(gpu, name)
+    W, H = sc.width, sc.height
+    t = gpu.Tracer(sc, W, H, mode)
+    cold = t.render()
+    for _ in range(2):
+        assert np.array_equal(t.render(), cold)
+    for world in (3, 8):
+        for _ in range(2):
+            assert np.array_equal(gpu.render_dist_sim(sc, W, H, mode, world), cold)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("w,h,world", [(37, 29, 3), (24, 5, 8), (64, 61, 2)])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_dist_path_odd_frames(gpu, w, h, world, mode):

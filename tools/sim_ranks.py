@@ -138,7 +138,9 @@ def product_ranks(args):
     """Every rank's share through the product's rank path on this GPU
     (rt_test_dist_sim_rank: rt_render_dist's dist_frame with the RCCL gather
     replaced by a device copy; rank 0 also places/decodes every slot).  The
-    exposed gather is modelled as the last chunk's bytes over one xGMI link."""
+    frame ends at the later of rank 0's own timeline and the slowest other
+    rank + its last chunk's bytes over one xGMI link + that chunk's placement
+    on rank 0 (timed)."""
     text, mode = scenes.config_json(args.config)
     sc = rtamd.load_scene_from_json_text(text)
     W, H = sc.width, sc.height
@@ -167,23 +169,49 @@ def product_ranks(args):
         worst = max(p["wall_ms"] for p in per)
         if base is None and N == 1:
             base = worst
-        rows = rtamd.dist_rows(H, N, 0, mode)
+        m = max(len(rtamd.dist_rows(H, N, r, mode)) for r in range(N))   # rows per rank slot (dist_frame's m)
         strip = frame_dist.strip_for(mode)
         nch = int(os.environ.get("RT_DIST_CHUNKS_PAPER" if mode == 1 else "RT_DIST_CHUNKS", "4"))
-        a_last, b_last = frame_dist.chunk_bounds(len(rows), max(1, min(4, nch)), strip)[-1]
+        a_last, b_last = frame_dist.chunk_bounds(m, max(1, min(4, nch)), strip)[-1]
         bpp = 1 if mode == 1 else (3 if args.rgb8 else 24)   # paper: one code byte per pixel
         last_chunk = (b_last - a_last) * W * bpp
-        g64 = last_chunk / 64e9 * 1e3 if N > 1 else 0.0
-        g153 = last_chunk / 153e9 * 1e3 if N > 1 else 0.0
+        # the last chunk's placement on rank 0 can only start once the slowest
+        # rank's gather has landed: timed as the same row scatter over N * the
+        # last chunk's rows (24 B/px read + written), scaled to what the product
+        # moves (FP64: 24 + 24 B/px; paper codes: 1 + 24; RGB8: 3 + 3)
+        place_ms = 0.0
+        if N > 1:
+            row_bytes = W * 24
+            n_slots = max(1, (b_last - a_last) * N)
+            src = rtamd.DeviceBuffer(n_slots * row_bytes)
+            rows_d = rtamd.DeviceBuffer(n_slots * 4)
+            rows_d.from_host(np.arange(n_slots, dtype=np.int32) % H)
+            dst = rtamd.DeviceBuffer(H * row_bytes)
+            lib.rt_scatter_rows_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+            lib.rt_scatter_rows_device(src.ptr, rows_d.ptr, n_slots, W, dst.ptr, None)
+            rtamd.device_synchronize()
+            tc = time.perf_counter()
+            for _ in range(5):
+                lib.rt_scatter_rows_device(src.ptr, rows_d.ptr, n_slots, W, dst.ptr, None)
+            rtamd.device_synchronize()
+            place_ms = (time.perf_counter() - tc) / 5 * 1e3 * (bpp + (3 if args.rgb8 else 24)) / 48.0
+        others = max((p["wall_ms"] for p in per[1:]), default=0.0)
+
+        def frame_ms(rate):   # rank 0's own timeline vs. the slowest peer + its last gather + placement
+            if N == 1:
+                return worst
+            return max(per[0]["wall_ms"], others + last_chunk / rate * 1e3 + place_ms)
+        t64, t153 = frame_ms(64e9), frame_ms(153e9)
         out = {"config": args.config, "world": N, "path": "product rank (rt_test_dist_sim_rank)", "chunks": nch,
                "max_rank_wall_ms": round(worst, 3), "rank0_wall_ms": round(per[0]["wall_ms"], 3),
                "min_rank_wall_ms": round(min(p["wall_ms"] for p in per), 3),
                "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
-               "gather_bytes_per_rank": len(rows) * W * bpp,
+               "gather_bytes_per_rank": m * W * bpp,
                "speedup_before_gather": round(base / worst, 3) if base else None,
-               "exposed_gather_ms_64GBs": round(g64, 4), "exposed_gather_ms_153GBs": round(g153, 4),
-               "projected_speedup_64GBs": round(base / (worst + g64), 3) if base else None,
-               "projected_speedup_153GBs": round(base / (worst + g153), 3) if base else None}
+               "last_chunk_place_ms": round(place_ms, 4),
+               "frame_ms_64GBs": round(t64, 4), "frame_ms_153GBs": round(t153, 4),
+               "projected_speedup_64GBs": round(base / t64, 3) if base else None,
+               "projected_speedup_153GBs": round(base / t153, 3) if base else None}
         print(json.dumps(out), flush=True)
 
 
