@@ -83,14 +83,19 @@ int rt_test_dist_create_rccl1(struct rt_dist** out);
  * trace fails at its middle chunk, 2 = the collective stream is held past the
  * rank's timeout (bounded: the holding kernel always ends). */
 int rt_test_dist_inject(struct rt_dist* d, int what);
-/* GPU: one simulated rank (rank of world) of a distributed frame on the
- * current device through the product's rank path, the RCCL gather replaced by
- * a device copy (rank 0 also places every slot).  Ranks are cached, so a
- * repeated call times a warm rank.  For per-rank timing (tools/sim_ranks.py). */
 /* CPU: the paper-mode output code decoder of distributed frames
  * (rtamd::paper_code_value): bits 0-2 edge index in {0, 0.3, 0.5, 0.6, 0.9},
  * bit 3 halved at the frame border, bit 4 the hatch bit (white). */
 double rt_test_paper_code_value(int code);
+/* CPU: the paper-mode primary launch order (rt_render.hip order_paper_groups)
+ * applied in place to list[0, n) (n a multiple of 16; entries are ext
+ * indices, -1 padding), given the measured cost of the 8-entry group whose
+ * first entry is e in cost[e] (0 = unmeasured).  Returns 0. */
+int rt_test_paper_order(int32_t* list, int n, const uint32_t* cost, int n_cost);
+/* GPU: one simulated rank (rank of world) of a distributed frame on the
+ * current device through the product's rank path, the RCCL gather replaced by
+ * a device copy (rank 0 also places every slot).  Ranks are cached, so a
+ * repeated call times a warm rank.  For per-rank timing (tools/sim_ranks.py). */
 int rt_test_dist_sim_rank(const struct rt_scene* s, int W, int H, int mode, int flags, int world, int rank, int rgb8,
                           struct rt_stats* stats);
 

@@ -169,6 +169,10 @@ __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_
     std_body<false, false, true, C, false, WV>(S, P);   // (no directional lights: those scenes take D)
 }
 
+// Paper-mode primary records: the material slot of a pixel whose ray hit
+// nothing (a hit's material is an index >= 0, or -1 for none).
+constexpr int kPaperMiss = -3;
+
 // A primary wave's (start, end) tick slot: group-major, 2 * gridDim.x waves
 // (8-column tiles) per 8-entry list group.
 __device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
@@ -213,12 +217,11 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         else
             hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
         idx = (size_t)ei * P.W + x;
-        P.hit[idx] = hits ? 1 : 0;
         P.t[idx] = ht;
         P.nx[idx] = h.n.x;
         P.ny[idx] = h.n.y;
         P.nz[idx] = h.n.z;
-        P.mat[idx] = hits ? h.mat : -3;
+        P.mat[idx] = hits ? h.mat : kPaperMiss;   // (the finish pass's hit flag)
         sh = P.ext_shade[ei] != 0;   // (a neighbour-only row needs the hit, not the shading)
     }
     // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125).  shade()
@@ -275,11 +278,29 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     if (x >= P.W || ri >= P.n_rows) return;
     const int y = P.rows[ri];
     const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
+    // Every operand is loaded up front, in one round of independent loads:
+    // neighbours outside the frame are clamped onto the centre and skipped
+    // below, and hit/miss is mat != kPaperMiss (the primary pass stores that
+    // sentinel for a miss), so the kernel no longer waits on a hit flag
+    // before fetching t and n.
     const size_t ci = (size_t)e_c * P.W + x;
-    const bool ch = P.hit[ci] != 0;
+    const size_t nidx[4] = {ci - (x > 0 ? 1 : 0), ci + (x + 1 < P.W ? 1 : 0),
+                            (size_t)(e_up >= 0 ? e_up : e_c) * P.W + x, (size_t)(e_dn >= 0 ? e_dn : e_c) * P.W + x};
+    const int cm = P.mat[ci];
     const real ct = P.t[ci];
     const V3 cn = v3(P.nx[ci], P.ny[ci], P.nz[ci]);
-    const int cm = P.mat[ci];
+    const real clum = P.lum[ci];
+    int nm[4];
+    real nt[4], nnx[4], nny[4], nnz[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        nm[i] = P.mat[nidx[i]];
+        nt[i] = P.t[nidx[i]];
+        nnx[i] = P.nx[nidx[i]];
+        nny[i] = P.ny[nidx[i]];
+        nnz[i] = P.nz[nidx[i]];
+    }
+    const bool ch = cm != kPaperMiss;
     // get_edge_strength (tracer.cpp:133-178): neighbours (-1,0) (1,0) (0,-1) (0,1)
     real maxEdge = RV(0.0);
     int eidx = 0;   // index of maxEdge in {0, 0.3, 0.5, 0.6, 0.9} (rtamd::paper_code)
@@ -291,27 +312,24 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
         const int nxp = x + dx, nyp = y + dy;
         if (nxp < 0 || nxp >= P.W || nyp < 0 || nyp >= P.H) continue;
         ++valid;
-        const int er = (dy < 0) ? e_up : (dy > 0) ? e_dn : e_c;
-        const size_t ni = (size_t)er * P.W + nxp;
-        const bool nh = P.hit[ni] != 0;
+        const bool nh = nm[i] != kPaperMiss;
         if (ch != nh) {
             maxEdge = dmax(maxEdge, RV(0.9));
             eidx = max(eidx, 4);
             continue;
         }
         if (ch && nh) {
-            const real nt = P.t[ni];
-            const real minD = dmin(ct, nt), maxD = dmax(ct, nt);
+            const real minD = dmin(ct, nt[i]), maxD = dmax(ct, nt[i]);
             if (minD > RV(1e-4) && maxD / minD > RV(3.0)) {
                 maxEdge = dmax(maxEdge, RV(0.6));
                 eidx = max(eidx, 3);
             }
-            const real nd = dot3(cn, v3(P.nx[ni], P.ny[ni], P.nz[ni]));
+            const real nd = dot3(cn, v3(nnx[i], nny[i], nnz[i]));
             if (nd < RV(0.2)) {
                 maxEdge = dmax(maxEdge, RV(0.5));
                 eidx = max(eidx, 2);
             }
-            if (cm != P.mat[ni] && nd < RV(0.7)) {
+            if (cm != nm[i] && nd < RV(0.7)) {
                 maxEdge = dmax(maxEdge, RV(0.3));
                 eidx = max(eidx, 1);
             }
@@ -322,7 +340,7 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     if constexpr (CODES) {
         // distributed frames: the pixel's place in the output alphabet
         // (rtamd::paper_code), decoded bit-exactly on the root after the gather
-        const bool h = edge <= RV(0.5) && crosshatch(P.lum[ci], x, y) != RV(0.0);
+        const bool h = edge <= RV(0.5) && crosshatch(clum, x, y) != RV(0.0);
         P.code[(size_t)ri * P.W + x] = (uint8_t)(eidx | (valid < 4 ? 8 : 0) | (h ? 16 : 0));
         return;
     }
@@ -332,7 +350,7 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     } else if (edge > RV(0.5)) {
         o = v3(RV(0.2), RV(0.2), RV(0.2));
     } else {
-        const real h = crosshatch(P.lum[ci], x, y);
+        const real h = crosshatch(clum, x, y);
         o = v3(h, h, h);
         if (edge > RV(0.3)) {
             const real darken = (edge - RV(0.3)) * RV(0.4);

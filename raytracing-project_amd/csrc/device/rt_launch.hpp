@@ -109,8 +109,7 @@ struct PaperParams {
     const int32_t* ext_shade;    // 1 = row is rendered by this call (shade it)
     const int32_t* nbr;          // per rendered row: ext index of r-1, r, r+1 (-1 = outside frame)
     const int32_t* rows;         // rendered rows
-    int* hit;                    // [n_ext*W]
-    int* mat;
+    int* mat;                    // [n_ext*W]: material of the primary hit, kPaperMiss for none
     double* t;
     double* nx;
     double* ny;

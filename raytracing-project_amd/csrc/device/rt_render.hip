@@ -618,7 +618,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(ws.gtime.ensure((size_t)3 * f->n_ext * paper_waves_per_group(W) * 2 * sizeof(unsigned)));
         HIP_TRY(rtamd::upload_async(&ws.up, ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), st));
         const size_t npx = (size_t)f->n_ext * W;
-        HIP_TRY(ws.paper_i.ensure(npx * 2 * sizeof(int)));
+        HIP_TRY(ws.paper_i.ensure(npx * sizeof(int)));
         HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
     }
     HIP_TRY(hipEventRecord(ws.ev[1], st));
@@ -715,8 +715,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
         P.n_list = (int)list.size();
         P.n_rows = n;
         const size_t npx = (size_t)n_ext * W;
-        P.hit = ws.paper_i.as<int>();
-        P.mat = P.hit + npx;
+        P.mat = ws.paper_i.as<int>();
         double* dd = ws.paper_d.as<double>();
         P.t = dd;
         P.nx = dd + npx;
@@ -1057,6 +1056,15 @@ extern "C" int rt_framebuffer_to_rgb8_device(const double* fb_dev, size_t n_pixe
 
 // ------------------------------------------------------------- test hooks
 #include "rt_test.h"
+
+extern "C" int rt_test_paper_order(int32_t* list, int n, const uint32_t* cost, int n_cost) {
+    if (n < 0 || n % 16 || (n && !list) || n_cost < 0 || (n_cost && !cost)) return RT_ERR_INVALID_ARG;
+    std::vector<int32_t> L(list, list + n);
+    const std::vector<uint32_t> c(cost, cost + n_cost);
+    order_paper_groups(L, &c);
+    std::copy(L.begin(), L.end(), list);
+    return RT_OK;
+}
 
 extern "C" int rt_test_mt_jump_cpu(int K_blocks, int levels) {
     // Every radix-R tree polynomial x^(624*K*m*R^j) applied to the seed

@@ -220,3 +220,55 @@ def test_paper_code_decoder_matches_reference_expression(rt):
                 assert struct.pack("<d", got) == struct.pack("<d", want), (i, half, h, got, want)
                 seen.add(got)
     assert {0.0, 0.2, 1.0} <= seen and len(seen) >= 5   # incl. the darkened whites of edges 0.45 / 0.6*0.5...
+
+
+def test_paper_launch_order_permutes_whole_blocks(rt):
+    """rt_render.hip order_paper_groups: a paper frame's primary list is
+    relaunched in 16-entry blocks (one workgroup row), costliest first by the
+    previous frame's measured 8-entry group costs (keyed by each group's first
+    ext index), ties in list order, padding blocks last; any unmeasured group
+    keeps the whole list in row order."""
+    lib = rt.amd_lib()
+    lib.rt_test_paper_order.argtypes = [C.POINTER(C.c_int32), C.c_int, C.POINTER(C.c_uint32), C.c_int]
+    rng = np.random.default_rng(7)
+    n_ext = 96
+    # runs of consecutive ext rows padded to 8, the list padded to 16 (frame_trace)
+    lst = []
+    for a, b in [(0, 30), (30, 61), (61, 90), (90, 96)]:
+        while len(lst) % 8:
+            lst.append(-1)
+        lst.extend(range(a, b))
+    while len(lst) % 16:
+        lst.append(-1)
+    lst.extend([-1] * 16)   # an all-padding block
+    cost = np.zeros(n_ext, dtype=np.uint32)
+    groups = [lst[i:i + 8] for i in range(0, len(lst), 8)]
+    for g in groups:
+        e = next((v for v in g if v >= 0), -1)
+        if e >= 0:
+            cost[e] = rng.integers(1, 5)   # small values: ties happen
+
+    def run(lst, cost):
+        arr = (C.c_int32 * len(lst))(*lst)
+        c = (C.c_uint32 * len(cost))(*[int(v) for v in cost])
+        assert lib.rt_test_paper_order(arr, len(lst), c, len(cost)) == 0
+        return list(arr)
+
+    got = run(lst, cost)
+    blocks = [lst[i:i + 16] for i in range(0, len(lst), 16)]
+
+    def bcost(b):
+        s = 0
+        for g in (b[:8], b[8:]):
+            e = next((v for v in g if v >= 0), -1)
+            s += int(cost[e]) if e >= 0 else 0
+        return s
+    want = [v for b in sorted(blocks, key=lambda b: -bcost(b)) for v in b]   # (sorted is stable)
+    assert got == want
+    assert sorted(got) == sorted(lst) and got[-16:] == [-1] * 16
+    # one unmeasured group: row order kept
+    cost2 = cost.copy()
+    cost2[next(v for v in lst if v >= 0)] = 0
+    assert run(lst, cost2) == lst
+    # bad arguments
+    assert lib.rt_test_paper_order((C.c_int32 * 8)(), 8, (C.c_uint32 * 1)(), 1) != 0
