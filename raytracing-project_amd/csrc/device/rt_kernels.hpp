@@ -268,40 +268,15 @@ __device__ __forceinline__ real crosshatch(real lum, int x, int y) {
     return draw ? RV(0.0) : RV(1.0);
 }
 
-// CODES: a distributed frame's rank writes paper_code bytes (P.code) instead
-// of FP64 pixels (separate instance, so the one-GPU kernel carries none of
-// the code bookkeeping).
+// One paper pixel (tracer.cpp:258-281) from its primary record and its four
+// neighbours' (-1,0) (1,0) (0,-1) (0,1), already loaded.  CODES: a
+// distributed frame's rank writes a paper_code byte (P.code) instead of FP64.
 template <bool CODES>
-__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= P.W || ri >= P.n_rows) return;
-    const int y = P.rows[ri];
-    const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
-    // Every operand is loaded up front, in one round of independent loads:
-    // neighbours outside the frame are clamped onto the centre and skipped
-    // below, and hit/miss is mat != kPaperMiss (the primary pass stores that
-    // sentinel for a miss), so the kernel no longer waits on a hit flag
-    // before fetching t and n.
-    const size_t ci = (size_t)e_c * P.W + x;
-    const size_t nidx[4] = {ci - (x > 0 ? 1 : 0), ci + (x + 1 < P.W ? 1 : 0),
-                            (size_t)(e_up >= 0 ? e_up : e_c) * P.W + x, (size_t)(e_dn >= 0 ? e_dn : e_c) * P.W + x};
-    const int cm = P.mat[ci];
-    const real ct = P.t[ci];
-    const V3 cn = v3(P.nx[ci], P.ny[ci], P.nz[ci]);
-    const real clum = P.lum[ci];
-    int nm[4];
-    real nt[4], nnx[4], nny[4], nnz[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        nm[i] = P.mat[nidx[i]];
-        nt[i] = P.t[nidx[i]];
-        nnx[i] = P.nx[nidx[i]];
-        nny[i] = P.ny[nidx[i]];
-        nnz[i] = P.nz[nidx[i]];
-    }
+__device__ __forceinline__ void paper_pixel(const PaperParams& P, int x, int y, int ri, int cm, real ct, V3 cn,
+                                            real clum, const int (&nm)[4], const real (&nt)[4], const real (&nnx)[4],
+                                            const real (&nny)[4], const real (&nnz)[4]) {
     const bool ch = cm != kPaperMiss;
-    // get_edge_strength (tracer.cpp:133-178): neighbours (-1,0) (1,0) (0,-1) (0,1)
+    // get_edge_strength (tracer.cpp:133-178)
     real maxEdge = RV(0.0);
     int eidx = 0;   // index of maxEdge in {0, 0.3, 0.5, 0.6, 0.9} (rtamd::paper_code)
     int valid = 0;
@@ -363,6 +338,77 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
     dst[0] = o.x;
     dst[1] = o.y;
     dst[2] = o.z;
+}
+
+// The finish pass: 64x4 threads per block.  Every operand is loaded up front
+// in one round of independent loads (neighbours outside the frame clamped
+// onto the centre and skipped by paper_pixel; hit/miss is the material slot
+// against kPaperMiss).  PAIR (even W): a thread takes two adjacent pixels
+// with 8/16-byte loads of both, and their outer x-neighbours.
+template <bool CODES, bool PAIR>
+__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
+    const int xt = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int x = PAIR ? 2 * xt : xt;
+    if (x >= P.W || ri >= P.n_rows) return;
+    const int y = P.rows[ri];
+    const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
+    const size_t ci = (size_t)e_c * P.W + x;
+    const size_t ui = (size_t)(e_up >= 0 ? e_up : e_c) * P.W + x, di = (size_t)(e_dn >= 0 ? e_dn : e_c) * P.W + x;
+    if constexpr (!PAIR) {
+        const size_t nidx[4] = {ci - (x > 0 ? 1 : 0), ci + (x + 1 < P.W ? 1 : 0), ui, di};
+        int nm[4];
+        real nt[4], nnx[4], nny[4], nnz[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            nm[i] = P.mat[nidx[i]];
+            nt[i] = P.t[nidx[i]];
+            nnx[i] = P.nx[nidx[i]];
+            nny[i] = P.ny[nidx[i]];
+            nnz[i] = P.nz[nidx[i]];
+        }
+        paper_pixel<CODES>(P, x, y, ri, P.mat[ci], P.t[ci], v3(P.nx[ci], P.ny[ci], P.nz[ci]), P.lum[ci], nm, nt, nnx,
+                           nny, nnz);
+    } else {
+        // rows: c = centre, u = up, d = down; pixels x and x + 1 (x even, W even:
+        // every pair is 8/16-byte aligned)
+        const int2 mc = *reinterpret_cast<const int2*>(P.mat + ci);
+        const int2 mu = *reinterpret_cast<const int2*>(P.mat + ui);
+        const int2 md = *reinterpret_cast<const int2*>(P.mat + di);
+        const double2 tc = *reinterpret_cast<const double2*>(P.t + ci);
+        const double2 tu = *reinterpret_cast<const double2*>(P.t + ui);
+        const double2 td = *reinterpret_cast<const double2*>(P.t + di);
+        const double2 xc = *reinterpret_cast<const double2*>(P.nx + ci);
+        const double2 xu = *reinterpret_cast<const double2*>(P.nx + ui);
+        const double2 xd = *reinterpret_cast<const double2*>(P.nx + di);
+        const double2 yc = *reinterpret_cast<const double2*>(P.ny + ci);
+        const double2 yu = *reinterpret_cast<const double2*>(P.ny + ui);
+        const double2 yd = *reinterpret_cast<const double2*>(P.ny + di);
+        const double2 zc = *reinterpret_cast<const double2*>(P.nz + ci);
+        const double2 zu = *reinterpret_cast<const double2*>(P.nz + ui);
+        const double2 zd = *reinterpret_cast<const double2*>(P.nz + di);
+        const double2 lc = *reinterpret_cast<const double2*>(P.lum + ci);
+        const size_t li = ci - (x > 0 ? 1 : 0), rj = ci + 1 + (x + 2 < P.W ? 1 : 0);
+        const int ml = P.mat[li], mr = P.mat[rj];
+        const real tl = P.t[li], tr = P.t[rj];
+        const real xl = P.nx[li], xr = P.nx[rj], yl = P.ny[li], yr = P.ny[rj], zl = P.nz[li], zr = P.nz[rj];
+        {
+            const int nm[4] = {ml, mc.y, mu.x, md.x};
+            const real nt[4] = {tl, RV(tc.y), RV(tu.x), RV(td.x)};
+            const real nnx[4] = {xl, RV(xc.y), RV(xu.x), RV(xd.x)}, nny[4] = {yl, RV(yc.y), RV(yu.x), RV(yd.x)},
+                       nnz[4] = {zl, RV(zc.y), RV(zu.x), RV(zd.x)};
+            paper_pixel<CODES>(P, x, y, ri, mc.x, RV(tc.x), v3(RV(xc.x), RV(yc.x), RV(zc.x)), RV(lc.x), nm, nt, nnx,
+                               nny, nnz);
+        }
+        {
+            const int nm[4] = {mc.x, mr, mu.y, md.y};
+            const real nt[4] = {RV(tc.x), tr, RV(tu.y), RV(td.y)};
+            const real nnx[4] = {RV(xc.x), xr, RV(xu.y), RV(xd.y)}, nny[4] = {RV(yc.x), yr, RV(yu.y), RV(yd.y)},
+                       nnz[4] = {RV(zc.x), zr, RV(zu.y), RV(zd.y)};
+            paper_pixel<CODES>(P, x + 1, y, ri, mc.y, RV(tc.y), v3(RV(xc.y), RV(yc.y), RV(zc.y)), RV(lc.y), nm, nt, nnx,
+                               nny, nnz);
+        }
+    }
 }
 
 // bv: the wave BVH kernels, whose object list is the Morton-ordered one
@@ -510,8 +556,15 @@ const void* paper_kernel(bool e, bool d, bool wv, bool bv) {
 }
 
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {
-    if (P.code) hipLaunchKernelGGL(k_paper_finish<true>, grid, dim3(256), 0, st, P);
-    else hipLaunchKernelGGL(k_paper_finish<false>, grid, dim3(256), 0, st, P);
+    // (grid.x covers W pixels one per thread; even W: two per thread)
+    if (P.W % 2 == 0) {
+        const dim3 g2((P.W / 2 + 63) / 64, grid.y);
+        if (P.code) hipLaunchKernelGGL((k_paper_finish<true, true>), g2, dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((k_paper_finish<false, true>), g2, dim3(256), 0, st, P);
+    } else {
+        if (P.code) hipLaunchKernelGGL((k_paper_finish<true, false>), grid, dim3(256), 0, st, P);
+        else hipLaunchKernelGGL((k_paper_finish<false, false>), grid, dim3(256), 0, st, P);
+    }
 }
 
 }  // namespace RT_NS
