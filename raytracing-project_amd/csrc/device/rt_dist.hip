@@ -472,12 +472,16 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     }
     if (!coll && rc != RT_OK) return rc;
 
-    // agreement 1 (collective frames): descriptor + setup status of every rank
+    // agreement 1 (collective frames): descriptor + setup status of every
+    // rank, issued right after chunk 0's trace is enqueued (so that the
+    // trace starts without waiting for these host calls) and awaited before
+    // the first gather.  A failure of chunk 0's own launch is reported here
+    // too.
     int64_t* xd = D.xchg.as<int64_t>();
     int64_t* xh = D.xchg_host;
     const size_t n_desc = 2 * kDescFields + (size_t)D.world;
     bool agreed = !coll;
-    if (coll) {
+    auto issue_agreement = [&]() -> bool {
         const int64_t v[kDescFields] = {W, H, mode, kind, flags};
         for (int i = 0; i < kDescFields; ++i) {
             xh[i] = v[i];
@@ -502,9 +506,9 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             if (f) (void)rt_frame_end(f, nullptr);
             dist_abort(D, "frame agreement could not be issued");
             rtamd::set_last_error("rt_render_dist: the frame agreement could not be issued; communicator aborted");
-            return RT_ERR_HIP;
         }
-    }
+        return ok;
+    };
     double* fb_rows = direct ? static_cast<double*>(out_root) : D.mine.as<double>();
     int n_tb = 0, n_g = 0;
     bool status_sent = false;
@@ -533,7 +537,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             continue;
         }
         if (!agreed) {
-            // the descriptor reduction ran while chunk 0 was being traced
+            if (!issue_agreement()) return RT_ERR_HIP;
+            // (the descriptor reduction runs while chunk 0 traces)
             const int rw = dist_wait(D, D.ev_desc, "the frame agreement");
             if (rw != RT_OK) {
                 if (f) (void)rt_frame_end(f, nullptr);
@@ -557,7 +562,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
                     rtamd::set_last_error("rt_render_dist: the ranks disagree on the frame (" + bad + ")");
                     return RT_ERR_INVALID_ARG;
                 }
-                rtamd::set_last_error("rt_render_dist: rank(s) " + failed + " failed to set up the frame");
+                rtamd::set_last_error("rt_render_dist: rank(s) " + failed + " failed to set up or start the frame");
                 return RT_ERR_HIP;
             }
             agreed = true;
