@@ -150,6 +150,18 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
                                       start_new_session=True))
+    # the ranks run in their own sessions (a terminal's job-control signals do
+    # not reach them), so a SIGTERM / SIGINT to this process stops them first
+    import signal
+
+    def _stop(signum, frame):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        signal.signal(signum, signal.SIG_DFL)
+        os.kill(os.getpid(), signum)
+
+    old_handlers = {sig: signal.signal(sig, _stop) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
     try:
         live = list(range(n))
@@ -171,8 +183,10 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
             if p.poll() is None:
                 p.kill()
                 p.wait()
-        try:   # the id file, if rank 0 did not get to remove it
-            os.unlink(os.path.join(tempfile.gettempdir(), f"rtamd_uid_{port}_{run_id}"))
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
+        try:   # the id file (rendezvous._path: port, the ranks' parent = this process, run id)
+            os.unlink(os.path.join(tempfile.gettempdir(), f"rtamd_uid_{port}_{os.getpid()}_{run_id}"))
         except FileNotFoundError:
             pass
     return rc

@@ -64,12 +64,49 @@ int rt_test_div3(const double* a_host, const double* b_host, int n, double* div3
  * Returns 0 equal, 1 different, 2 file missing / short / corrupt. */
 int rt_test_mt_poly_file(const char* path, int levels);
 
-/* GPU, one device: the multi-GPU frame path of rt_render_multi /
- * rt_render_dist (partition, row chunks, gather stage layout, placement on
- * the root) with `world` simulated ranks rendered one after another on the
- * current device and the RCCL gather replaced by device copies into the same
- * stage.  Writes the root's frame to fb_host (W*H*3 doubles) or, with rgb8,
- * its bytes to rgb8_host.  For tests on one-GPU machines. */
+/* GPU, one device: the distributed frame of rt_render_dist with `world`
+ * (<= 16) simulated ranks running CONCURRENTLY on the current device, one
+ * host thread per rank with its own streams and device workspace, through the
+ * product's rank path (dist_frame) with RCCL replaced by a same-device
+ * transport that keeps its contract (host rendezvous + device copies / max
+ * reduction on each rank's collective stream, timeouts): partition, row
+ * chunks, both frame agreements and their verdicts, gathers, placement on the
+ * root.  run->frames consecutive frames; in frame run->fault_frame rank
+ * run->fault_rank gets run->fault:
+ *   TRACE       its trace fails at its middle chunk (after the agreement)
+ *   SETUP       it fails before its frame begins (reported in the agreement)
+ *   DESC_H      it is given H + 1 (the ranks disagree on the descriptor)
+ *   DESC_FLAGS  it is given flags ^ RT_FLAG_NO_CULL
+ *   ABSENT      it does not take part in that frame (a dead peer; the others
+ *               time out after run->timeout_ms)
+ * Per frame fr and rank r: run->rc[fr*world + r] (an rt_status, or
+ * RT_TEST_RANK_ABSENT), run->ms[...] (the call's wall time), and the error
+ * text in run->msgs[(fr*world + r) * msg_cap ...] (may be NULL).  The root's
+ * frame of every successful frame fr goes to fb_host + fr*W*H*3 (doubles) or,
+ * with run->rgb8, rgb8_host + fr*W*H*3 (either may be NULL).  timeout_ms <= 0:
+ * RT_DIST_TIMEOUT_MS / 120 s.  Returns an rt_status for the harness itself. */
+enum {
+    RT_TEST_FAULT_NONE = 0,
+    RT_TEST_FAULT_TRACE = 1,
+    RT_TEST_FAULT_SETUP = 2,
+    RT_TEST_FAULT_DESC_H = 3,
+    RT_TEST_FAULT_DESC_FLAGS = 4,
+    RT_TEST_FAULT_ABSENT = 5
+};
+#define RT_TEST_RANK_ABSENT 1
+typedef struct rt_test_dist_run {
+    int world, rgb8, frames;
+    int fault_rank, fault, fault_frame;
+    int timeout_ms;
+    int msg_cap;
+    int* rc;
+    double* ms;
+    char* msgs;
+} rt_test_dist_run;
+int rt_test_dist_threads(const struct rt_scene* s, int W, int H, int mode, int flags, rt_test_dist_run* run,
+                         double* fb_host, uint8_t* rgb8_host);
+/* rt_test_dist_threads for one fault-free frame: the root's frame to fb_host
+ * (W*H*3 doubles) or, with rgb8, rgb8_host. */
 int rt_test_render_dist_sim(const struct rt_scene* s, int W, int H, int mode, int flags, int world, int rgb8,
                             double* fb_host, uint8_t* rgb8_host);
 
@@ -81,7 +118,8 @@ struct rt_dist;
 int rt_test_dist_create_rccl1(struct rt_dist** out);
 /* Fault injection on the next frame of d (rt_render_dist): 1 = this rank's
  * trace fails at its middle chunk, 2 = the collective stream is held past the
- * rank's timeout (bounded: the holding kernel always ends). */
+ * rank's timeout (bounded, >= 10 s: the holding kernel always ends), 3 = this
+ * rank fails before its frame begins. */
 int rt_test_dist_inject(struct rt_dist* d, int what);
 /* CPU: the paper-mode output code decoder of distributed frames
  * (rtamd::paper_code_value): bits 0-2 edge index in {0, 0.3, 0.5, 0.6, 0.9},

@@ -25,7 +25,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -236,6 +238,91 @@ hipError_t place_codes(const uint8_t* src, const int32_t* rows_dev, int n_slots,
     return hipGetLastError();
 }
 
+// ------------------------------------------------------ test transport
+// rt_test_dist_threads: the ranks of a distributed frame simulated on ONE
+// device, concurrently, one host thread per rank with its own streams and its
+// own device workspace (as separate processes would have them).  Their
+// collectives keep RCCL's contract - every rank issues the same sequence, and
+// each collective is ordered on the rank's collective stream - through host
+// rendezvous plus device work on the ranks' own streams:
+//   all-reduce (max): each rank records "input ready"; rendezvous (input
+//     pointers posted); each rank waits for every input and reduces all of
+//     them into a private temporary, records "read"; rendezvous; each rank
+//     waits until every rank has read its input, then copies the temporary
+//     over its buffer (in place, as the agreement reductions use it).
+//   gather: each rank records "send ready"; rendezvous (send pointers
+//     posted); the root waits for every send and copies it into its receive
+//     buffer, records "copied"; rendezvous; the other ranks' streams wait for
+//     "copied" (a send completes once the root holds the data).
+// Every device wait refers to an event recorded before the rendezvous that
+// publishes it, so no stream can wait on work queued behind it.  A rendezvous
+// waits at most the rank's timeout: a rank that times out (a peer that never
+// arrives) or aborts marks the group aborted, and its peers see that as the
+// communicator's asynchronous error (dist_wait) or at their next rendezvous.
+constexpr int kSimMaxWorld = 16;
+
+struct SimGroup {
+    explicit SimGroup(int w) : world(w), posted((size_t)w, nullptr), in((size_t)w, nullptr), rd((size_t)w, nullptr) {}
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int count = 0;
+    uint64_t gen = 0;
+    bool aborted = false;
+    std::string why;
+    std::vector<const void*> posted;        // one pointer per rank, posted at a collective's first rendezvous
+    std::vector<hipEvent_t> in, rd;         // per rank: input / send ready, all-reduce inputs read
+    hipEvent_t copied = nullptr;            // the root's gather copies
+    // Rendezvous of every rank (post: this rank's pointer, or nullptr at a
+    // collective's second rendezvous).  Returns "" or why it failed.
+    std::string meet(int rank, const void* post, double timeout_ms, const char* what) {
+        std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return "the group was aborted (" + why + ")";
+        if (post) posted[rank] = post;
+        const uint64_t g = gen;
+        if (++count == world) {
+            count = 0;
+            ++gen;
+            cv.notify_all();
+            return "";
+        }
+        const bool done = cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms),
+                                      [&] { return gen != g || aborted; });
+        if (gen != g) return "";
+        if (!done) {
+            aborted = true;
+            why = "rank " + std::to_string(rank) + " timed out after " + std::to_string((long)timeout_ms) +
+                  " ms waiting for " + what + " (a peer rank did not take part)";
+            cv.notify_all();
+            return why;
+        }
+        return "the group was aborted (" + why + ")";
+    }
+    void abort(const std::string& w) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!aborted) why = w;
+        aborted = true;
+        cv.notify_all();
+    }
+    bool is_aborted(std::string* w) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (aborted && w) *w = why;
+        return aborted;
+    }
+};
+
+struct I64Ptrs {
+    const int64_t* p[kSimMaxWorld];
+};
+
+__global__ void k_sim_max_i64(I64Ptrs in, int world, int n, int64_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t v = in.p[0][i];
+    for (int r = 1; r < world; ++r) v = std::max(v, in.p[r][i]);
+    out[i] = v;
+}
+
 }  // namespace
 
 // One rank of a frame distribution (also the single-device case, world 1).
@@ -252,7 +339,9 @@ struct rt_dist {
     hipEvent_t ev_tb[2 * kChunks] = {};
     std::vector<int32_t> rowtab_host;          // source of the async row-table upload
     std::mutex mu;                            // one frame at a time per rank
-    DevBuf* sim_stage = nullptr;              // rt_test_render_dist_sim: shared stage, copies instead of RCCL
+    DevBuf* sim_stage = nullptr;              // rt_test_dist_sim_rank: shared stage, copies instead of RCCL
+    SimGroup* simg = nullptr;                 // rt_test_dist_threads: concurrent ranks, same-device transport
+    DevBuf simtmp;                            //   its all-reduce temporary
     bool force_collective = false;            // rt_test_dist_create_rccl1: world 1 through ncclGather
     DevBuf red;                               // rt_dist_reduce_max scratch
     // Per-frame agreement (collective frames): the frame descriptor + each
@@ -264,6 +353,8 @@ struct rt_dist {
     hipEvent_t ev_desc = nullptr;
     bool dead = false;                        // communicator aborted: the handle renders no more frames
     std::string dead_why;
+    std::thread abort_th;                     // ncclCommAbort runs here (it can wait for the stream to drain)
+    std::atomic<double> abort_ms{-1.0};       //   its duration once done
     double timeout_ms = 120000.0;             // RT_DIST_TIMEOUT_MS / rt_dist_set_timeout
     int inject = 0;                           // rt_test_dist_inject (next frame only)
     bool collective() const { return world > 1 || force_collective; }
@@ -312,16 +403,36 @@ int dist_init_xchg(rt_dist& D) {
     return RT_OK;
 }
 
+// The communicator is aborted on a helper thread: ncclCommAbort can wait
+// for work already queued on the collective stream (a held stream kept it
+// 1.9 s, gpurun_out/r04c_dist_tests.log), and the rank must return near its
+// deadline, not when its stream drains.  release_rank joins the thread; its
+// duration is reported with the handle's later refusals.
 void dist_abort(rt_dist& D, const std::string& why) {
-    const auto t0 = std::chrono::steady_clock::now();
-    if (D.comm && D.own_comm) (void)ncclCommAbort(D.comm);
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (D.simg) D.simg->abort("rank " + std::to_string(D.rank) + ": " + why);
+    if (D.comm && D.own_comm) {
+        if (D.abort_th.joinable()) D.abort_th.join();
+        ncclComm_t c = D.comm;
+        std::atomic<double>* ms = &D.abort_ms;
+        D.abort_th = std::thread([c, ms] {
+            const auto t0 = std::chrono::steady_clock::now();
+            (void)ncclCommAbort(c);
+            ms->store(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        });
+    }
     D.comm = nullptr;
     D.own_comm = false;
     D.dead = true;
-    char buf[64];
-    std::snprintf(buf, sizeof buf, " [ncclCommAbort %.1f ms]", ms);
-    D.dead_why = why + buf;
+    D.dead_why = why;
+}
+
+std::string abort_note(const rt_dist& D) {
+    const double ms = D.abort_ms.load();
+    if (!D.abort_th.joinable() && ms < 0) return "";
+    char buf[96];
+    if (ms < 0) std::snprintf(buf, sizeof buf, "; ncclCommAbort still running");
+    else std::snprintf(buf, sizeof buf, "; ncclCommAbort took %.1f ms", ms);
+    return buf;
 }
 
 int dist_wait(rt_dist& D, hipEvent_t ev, const char* what) {
@@ -339,21 +450,98 @@ int dist_wait(rt_dist& D, hipEvent_t ev, const char* what) {
                 const std::string why = std::string("RCCL asynchronous error during ") + what + ": " +
                                         ncclGetErrorString(ae);
                 dist_abort(D, why);
-                rtamd::set_last_error("rt_render_dist: " + why + " (communicator aborted)");
+                rtamd::set_last_error("rt_render_dist: " + why + " (communicator abort started)");
                 return RT_ERR_HIP;
             }
+        }
+        std::string gw;
+        if (D.simg && D.simg->is_aborted(&gw)) {
+            const std::string why = std::string("the group was aborted during ") + what + " (" + gw + ")";
+            dist_abort(D, why);
+            rtamd::set_last_error("rt_render_dist: " + why);
+            return RT_ERR_HIP;
         }
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (ms > D.timeout_ms) {
             const std::string why = std::string("timed out after ") + std::to_string((long)D.timeout_ms) +
                                     " ms waiting for " + what + " (a peer rank did not take part)";
             dist_abort(D, why);
-            rtamd::set_last_error("rt_render_dist: " + why + "; communicator aborted");
+            char buf[64];
+            std::snprintf(buf, sizeof buf, " (gave up at %.1f ms)", ms);
+            rtamd::set_last_error("rt_render_dist: " + why + buf + "; communicator abort started");
             return RT_ERR_HIP;
         }
         if (it < 4096) std::this_thread::yield();
         else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+}
+
+// The frame's collectives.  RCCL, or one of the two test stand-ins: the
+// concurrent same-device transport (D.simg, rt_test_dist_threads) and the
+// one-rank-at-a-time timing stand-in (D.sim_stage, rt_test_dist_sim_rank:
+// reductions are the identity, a gather is a copy into the shared stage).
+// Each returns "" or why it could not be issued.
+std::string coll_max_i64(rt_dist& D, int64_t* buf, size_t n, const char* what) {
+    if (D.sim_stage) return "";
+    if (D.simg) {
+        SimGroup& G = *D.simg;
+        const int w = G.world;
+        if (D.simtmp.ensure(n * sizeof(int64_t)) != hipSuccess) return "all-reduce temporary allocation failed";
+        if (hipEventRecord(G.in[D.rank], D.comm_st) != hipSuccess) return "event record failed";
+        std::string e = G.meet(D.rank, buf, D.timeout_ms, what);
+        if (!e.empty()) return e;
+        I64Ptrs P{};
+        for (int r = 0; r < w; ++r) {
+            P.p[r] = static_cast<const int64_t*>(G.posted[r]);
+            if (r != D.rank && hipStreamWaitEvent(D.comm_st, G.in[r], 0) != hipSuccess) return "stream wait failed";
+        }
+        hipLaunchKernelGGL(k_sim_max_i64, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, D.comm_st, P, w, (int)n,
+                           D.simtmp.as<int64_t>());
+        if (hipGetLastError() != hipSuccess || hipEventRecord(G.rd[D.rank], D.comm_st) != hipSuccess)
+            return "all-reduce launch failed";
+        e = G.meet(D.rank, nullptr, D.timeout_ms, what);
+        if (!e.empty()) return e;
+        for (int r = 0; r < w; ++r)
+            if (r != D.rank && hipStreamWaitEvent(D.comm_st, G.rd[r], 0) != hipSuccess) return "stream wait failed";
+        if (hipMemcpyAsync(buf, D.simtmp.p, n * sizeof(int64_t), hipMemcpyDeviceToDevice, D.comm_st) != hipSuccess)
+            return "all-reduce copy failed";
+        return "";
+    }
+    const ncclResult_t r = ncclAllReduce(buf, buf, n, ncclInt64, ncclMax, D.comm, D.comm_st);
+    return r == ncclSuccess ? "" : std::string("ncclAllReduce failed: ") + ncclGetErrorString(r);
+}
+
+// Gather `bytes` from every rank into recv (root only: world * bytes, rank
+// order).  bytes_type: the payload is bytes (RGB8 / paper codes), else doubles.
+std::string coll_gather(rt_dist& D, const void* send, void* recv, size_t bytes, bool bytes_type, const char* what) {
+    if (D.sim_stage) {
+        if (hipMemcpyAsync(static_cast<char*>(recv) + (size_t)D.rank * bytes, send, bytes, hipMemcpyDeviceToDevice,
+                           D.comm_st) != hipSuccess)
+            return "simulated gather copy failed";
+        return "";
+    }
+    if (D.simg) {
+        SimGroup& G = *D.simg;
+        if (hipEventRecord(G.in[D.rank], D.comm_st) != hipSuccess) return "event record failed";
+        std::string e = G.meet(D.rank, send, D.timeout_ms, what);
+        if (!e.empty()) return e;
+        if (D.rank == 0) {
+            for (int r = 0; r < G.world; ++r) {
+                if (r != 0 && hipStreamWaitEvent(D.comm_st, G.in[r], 0) != hipSuccess) return "stream wait failed";
+                if (bytes && hipMemcpyAsync(static_cast<char*>(recv) + (size_t)r * bytes, G.posted[r], bytes,
+                                            hipMemcpyDeviceToDevice, D.comm_st) != hipSuccess)
+                    return "gather copy failed";
+            }
+            if (hipEventRecord(G.copied, D.comm_st) != hipSuccess) return "event record failed";
+        }
+        e = G.meet(D.rank, nullptr, D.timeout_ms, what);
+        if (!e.empty()) return e;
+        if (D.rank != 0 && hipStreamWaitEvent(D.comm_st, G.copied, 0) != hipSuccess) return "stream wait failed";
+        return "";
+    }
+    const ncclResult_t r = ncclGather(send, D.rank == 0 ? recv : nullptr, bytes_type ? bytes : bytes / 8,
+                                      bytes_type ? ncclUint8 : ncclFloat64, 0, D.comm, D.comm_st);
+    return r == ncclSuccess ? "" : std::string("ncclGather failed: ") + ncclGetErrorString(r);
 }
 
 // rt_test_dist_inject: a kernel that holds the collective stream for a bounded
@@ -364,7 +552,7 @@ __global__ void k_test_stall(unsigned long long max_ticks) {
     while (wall_clock64() - t0 < max_ticks) __builtin_amdgcn_s_sleep(127);
 }
 
-enum { kInjectTraceFail = 1, kInjectStall = 2 };
+enum { kInjectTraceFail = 1, kInjectStall = 2, kInjectSetupFail = 3 };
 
 // Row chunks per rank and frame (each one gather): kChunks, or
 // RT_DIST_CHUNKS (standard mode) / RT_DIST_CHUNKS_PAPER from the environment
@@ -397,7 +585,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     std::lock_guard<std::mutex> lk(D.mu);
     if (D.dead) {
         rtamd::set_last_error("rt_render_dist: this rank's communicator was aborted (" + D.dead_why +
-                              "); destroy the handle and create a new one");
+                              abort_note(D) + "); destroy the handle and create a new one");
         return RT_ERR_HIP;
     }
     const bool root = D.rank == 0;
@@ -465,6 +653,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
                            hipMemcpyHostToDevice, D.comm_st) != hipSuccess)
             fail(RT_ERR_HIP, "placement table upload failed");
     }
+    if (rc == RT_OK && inject == kInjectSetupFail) fail(RT_ERR_HIP, "injected setup failure (rt_test_dist_inject)");
     rt_frame* f = nullptr;
     if (rc == RT_OK) {
         const int rb = rt_frame_begin(s, W, H, mode, flags, rows.data(), n, st, &f);
@@ -488,13 +677,20 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             xh[kDescFields + i] = -v[i];
         }
         for (int r = 0; r < D.world; ++r) xh[2 * kDescFields + r] = (r == D.rank && rc != RT_OK) ? 1 : 0;
+        std::string why;
         bool ok = hipMemcpyAsync(xd, xh, n_desc * sizeof(int64_t), hipMemcpyHostToDevice, D.comm_st) == hipSuccess;
-        if (ok && !D.sim_stage) ok = ncclAllReduce(xd, xd, n_desc, ncclInt64, ncclMax, D.comm, D.comm_st) == ncclSuccess;
+        if (!ok) why = "descriptor upload failed";
+        if (ok) {
+            why = coll_max_i64(D, xd, n_desc, "the frame agreement");
+            ok = why.empty();
+        }
         if (ok) ok = hipMemcpyAsync(xh, xd, n_desc * sizeof(int64_t), hipMemcpyDeviceToHost, D.comm_st) == hipSuccess;
         if (ok && inject == kInjectStall) {
             int rate_khz = 100000;
             (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, D.device);
-            const double stall_ms = std::min(D.timeout_ms * 4 + 1000, 10000.0);   // bounded: the wave always leaves
+            // bounded (the wave always leaves), and far longer than the timeout:
+            // the rank must give up at its deadline, not when the stream drains
+            const double stall_ms = std::min(std::max(10000.0, 4 * D.timeout_ms), 30000.0);
             const unsigned long long ticks = (unsigned long long)rate_khz * (unsigned long long)stall_ms;
             hipLaunchKernelGGL(k_test_stall, dim3(1), dim3(64), 0, D.comm_st, ticks);
             ok = hipGetLastError() == hipSuccess;
@@ -504,8 +700,10 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             // this rank cannot take part in the frame's collectives: its peers
             // will time out; abort so that nothing is left queued on them here
             if (f) (void)rt_frame_end(f, nullptr);
-            dist_abort(D, "frame agreement could not be issued");
-            rtamd::set_last_error("rt_render_dist: the frame agreement could not be issued; communicator aborted");
+            if (why.empty()) why = "HIP call failed";
+            dist_abort(D, "frame agreement could not be issued: " + why);
+            rtamd::set_last_error("rt_render_dist: the frame agreement could not be issued (" + why +
+                                  "); communicator aborted");
         }
         return ok;
     };
@@ -574,9 +772,10 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             int64_t* sh = xh + n_desc;
             for (int r = 0; r < D.world; ++r) sh[r] = (r == D.rank && rc != RT_OK) ? 1 : 0;
             bool ok = hipMemcpyAsync(sd, sh, n_stat * sizeof(int64_t), hipMemcpyHostToDevice, D.comm_st) == hipSuccess;
-            if (ok && !D.sim_stage) ok = ncclAllReduce(sd, sd, n_stat, ncclInt64, ncclMax, D.comm, D.comm_st) == ncclSuccess;
+            std::string why = ok ? coll_max_i64(D, sd, n_stat, "the trace status reduction") : "status upload failed";
+            ok = why.empty();
             if (ok) ok = hipMemcpyAsync(sh, sd, n_stat * sizeof(int64_t), hipMemcpyDeviceToHost, D.comm_st) == hipSuccess;
-            if (!ok) fail(RT_ERR_HIP, "trace status reduction could not be issued");
+            if (!ok) fail(RT_ERR_HIP, ("trace status reduction could not be issued: " + why).c_str());
             status_sent = ok;
         }
         // chunk k -> root: ONE collective, ordered after the chunk's trace
@@ -588,17 +787,12 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         const char* send = (kind && !codes ? D.mine8.as<char>() : D.mine.as<char>()) + (size_t)a * row_bytes;
         const size_t chunk_bytes = (size_t)(b - a) * row_bytes;
         char* recv = stage.as<char>() + (size_t)D.world * a * row_bytes;
-        if (D.sim_stage) {
-            if (hipMemcpyAsync(recv + (size_t)D.rank * chunk_bytes, send, chunk_bytes, hipMemcpyDeviceToDevice,
-                               D.comm_st) != hipSuccess)
-                fail(RT_ERR_HIP, "simulated gather copy failed");
-        } else {
-            const bool bytes = kind || codes;
-            const ncclResult_t r = ncclGather(send, root ? recv : nullptr, bytes ? chunk_bytes : chunk_bytes / 8,
-                                              bytes ? ncclUint8 : ncclFloat64, 0, D.comm, D.comm_st);
-            if (r != ncclSuccess) {
-                fail(RT_ERR_HIP, nullptr);
-                rtamd::set_last_error(std::string("rt_render_dist: ncclGather failed: ") + ncclGetErrorString(r));
+        {
+            const std::string why = coll_gather(D, send, (root || D.sim_stage) ? recv : nullptr, chunk_bytes,
+                                                kind || codes, "a gather");
+            if (!why.empty()) {
+                fail(RT_ERR_HIP, why.c_str());
+                if (D.simg && D.simg->is_aborted(nullptr)) dist_abort(D, why);
             }
         }
         if (root) {
@@ -660,6 +854,7 @@ void release_rank(rt_dist& d) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(d.device);
+    if (d.abort_th.joinable()) d.abort_th.join();
     if (d.comm_st) (void)hipStreamSynchronize(d.comm_st);
     if (d.comm && d.own_comm) (void)ncclCommDestroy(d.comm);
     d.comm = nullptr;
@@ -669,6 +864,7 @@ void release_rank(rt_dist& d) {
     d.stage.release();
     d.rowtab.release();
     d.red.release();
+    d.simtmp.release();
     d.xchg.release();
     if (d.xchg_host) (void)hipHostFree(d.xchg_host);
     d.xchg_host = nullptr;
@@ -942,35 +1138,136 @@ extern "C" int rt_render_dist_rgb8(rt_dist* d, const rt_scene* s, int W, int H, 
 }
 
 // ------------------------------------------------------------- test hook
-extern "C" int rt_test_render_dist_sim(const rt_scene* s, int W, int H, int mode, int flags, int world, int rgb8,
-                                       double* fb_host, uint8_t* rgb8_host) {
-    if (!s || W <= 0 || H <= 0 || world <= 0 || (rgb8 ? !rgb8_host : !fb_host)) return RT_ERR_INVALID_ARG;
+// The ranks of a distributed frame on the current device, CONCURRENTLY: one
+// host thread per rank, each with its own frame stream, collective and
+// alternate streams and device workspace (workspace slot rank + 1), through
+// dist_frame with the same-device transport (SimGroup) in place of RCCL, so
+// every line of the world >= 2 protocol runs: partition, chunks, the frame
+// agreement and trace-status reductions and their verdicts, gathers, the
+// root's placement, and the timeouts.  Ranks run their frames freely, as
+// processes would (no barrier between frames).  See rt_test.h.
+extern "C" int rt_test_dist_threads(const rt_scene* s, int W, int H, int mode, int flags, rt_test_dist_run* run,
+                                    double* fb_host, uint8_t* rgb8_host) {
+    if (!s || !run || W <= 0 || H <= 0 || run->world <= 0 || run->world > kSimMaxWorld || run->frames <= 0 ||
+        !run->rc || !run->ms)
+        return RT_ERR_INVALID_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
-    const size_t out_bytes = (size_t)W * H * 3 * (rgb8 ? 1 : sizeof(double));
-    DevBuf out, stage;
-    HIP_TRY(out.ensure(out_bytes));
-    HIP_TRY(hipMemset(out.p, 0xff, out_bytes));   // every byte must be written by the placement
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    const int world = run->world, frames = run->frames;
+    const int kind = run->rgb8 ? 1 : 0;
+    const size_t frame_bytes = (size_t)W * H * 3 * (kind ? 1 : sizeof(double));
+    DevBuf out;
+    HIP_TRY(out.ensure((size_t)W * (H + 1) * 3 * (kind ? 1 : sizeof(double))));   // (+1 row: a rank may be given H + 1)
+    SimGroup G(world);
     std::vector<std::unique_ptr<rt_dist>> ranks;
-    for (int r = 0; r < world; ++r) {
-        ranks.emplace_back(new rt_dist);
-        ranks.back()->world = world;
-        ranks.back()->rank = r;
-        ranks.back()->sim_stage = world > 1 ? &stage : nullptr;
-        HIP_TRY(hipGetDevice(&ranks.back()->device));
-    }
     int rc = RT_OK;
-    // non-root ranks first (they deposit their chunks), then the root places
-    for (int r = world - 1; r >= 0 && rc == RT_OK; --r) {
-        rt_stats st{};
-        rc = dist_frame(*ranks[r], s, W, H, mode, flags, rgb8 ? 1 : 0, r == 0 ? out.p : nullptr, nullptr, &st);
+    for (int r = 0; r < world && rc == RT_OK; ++r) {
+        ranks.emplace_back(new rt_dist);
+        rt_dist& D = *ranks.back();
+        D.world = world;
+        D.rank = r;
+        D.device = dev;
+        D.simg = world > 1 ? &G : nullptr;
+        D.timeout_ms = run->timeout_ms > 0 ? run->timeout_ms : env_timeout_ms();
+        if (hipEventCreateWithFlags(&G.in[r], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&G.rd[r], hipEventDisableTiming) != hipSuccess)
+            rc = RT_ERR_HIP;
     }
-    if (rc == RT_OK && hipMemcpy(rgb8 ? (void*)rgb8_host : (void*)fb_host, out.p, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
-        rc = RT_ERR_HIP;
+    if (rc == RT_OK && hipEventCreateWithFlags(&G.copied, hipEventDisableTiming) != hipSuccess) rc = RT_ERR_HIP;
+    if (rc == RT_OK) {
+        auto body = [&](int r) {
+            rt_dist& D = *ranks[r];
+            (void)hipSetDevice(dev);
+            rtamd::set_workspace_slot(r + 1);
+            hipStream_t st = nullptr;
+            const bool have_st = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+            for (int fr = 0; fr < frames; ++fr) {
+                const size_t o = (size_t)fr * world + r;
+                run->ms[o] = 0.0;
+                if (run->msgs && run->msg_cap > 0) run->msgs[o * run->msg_cap] = 0;
+                const bool hit = fr == run->fault_frame && r == run->fault_rank;
+                if (hit && run->fault == RT_TEST_FAULT_ABSENT) {
+                    run->rc[o] = RT_TEST_RANK_ABSENT;
+                    continue;
+                }
+                if (!have_st) {
+                    run->rc[o] = RT_ERR_HIP;
+                    continue;
+                }
+                int Hr = H, fl = flags;
+                if (hit) {
+                    if (run->fault == RT_TEST_FAULT_TRACE) D.inject = kInjectTraceFail;
+                    if (run->fault == RT_TEST_FAULT_SETUP) D.inject = kInjectSetupFail;
+                    if (run->fault == RT_TEST_FAULT_DESC_H) Hr = H + 1;
+                    if (run->fault == RT_TEST_FAULT_DESC_FLAGS) fl ^= RT_FLAG_NO_CULL;
+                }
+                if (r == 0) {   // every output byte must be written by this frame's placement
+                    (void)hipMemsetAsync(out.p, 0xff, out.n, st);
+                    (void)hipStreamSynchronize(st);
+                }
+                const auto t0 = std::chrono::steady_clock::now();
+                rt_stats stt{};
+                const int rr = dist_frame(D, s, W, Hr, mode, fl, kind, r == 0 ? out.p : nullptr, st, &stt);
+                run->ms[o] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                run->rc[o] = rr;
+                if (rr != RT_OK && run->msgs && run->msg_cap > 0)
+                    std::snprintf(run->msgs + o * run->msg_cap, (size_t)run->msg_cap, "%s", rt_last_error());
+                if (r == 0 && rr == RT_OK) {
+                    void* dst = kind ? (void*)(rgb8_host ? rgb8_host + (size_t)fr * frame_bytes : nullptr)
+                                     : (void*)(fb_host ? reinterpret_cast<char*>(fb_host) + (size_t)fr * frame_bytes : nullptr);
+                    if (dst && hipMemcpy(dst, out.p, frame_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+                        run->rc[o] = RT_ERR_HIP;
+                }
+            }
+            if (have_st) {
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
+            }
+            rtamd::set_workspace_slot(0);
+        };
+        std::vector<std::thread> th;
+        for (int r = 0; r < world; ++r) th.emplace_back(body, r);
+        for (auto& t : th) t.join();
+    }
+    (void)hipSetDevice(dev);
     for (auto& d : ranks) release_rank(*d);
-    stage.release();
+    for (hipEvent_t e : G.in) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : G.rd) if (e) (void)hipEventDestroy(e);
+    if (G.copied) (void)hipEventDestroy(G.copied);
     out.release();
+    (void)rtamd::release_device_workspaces(1);   // the simulated ranks' workspaces
+    (void)hipSetDevice(dev);
     return rc;
+}
+
+// ------------------------------------------------------------- test hook
+// rt_test_dist_threads for one fault-free frame (the root's frame only).
+extern "C" int rt_test_render_dist_sim(const rt_scene* s, int W, int H, int mode, int flags, int world, int rgb8,
+                                       double* fb_host, uint8_t* rgb8_host) {
+    if (!s || W <= 0 || H <= 0 || world <= 0 || world > kSimMaxWorld || (rgb8 ? !rgb8_host : !fb_host))
+        return RT_ERR_INVALID_ARG;
+    std::vector<int> rcs((size_t)world, RT_OK);
+    std::vector<double> ms((size_t)world, 0.0);
+    std::vector<char> msgs((size_t)world * 256, 0);
+    rt_test_dist_run run{};
+    run.world = world;
+    run.rgb8 = rgb8;
+    run.frames = 1;
+    run.fault_rank = -1;
+    run.rc = rcs.data();
+    run.ms = ms.data();
+    run.msgs = msgs.data();
+    run.msg_cap = 256;
+    const int rc = rt_test_dist_threads(s, W, H, mode, flags, &run, fb_host, rgb8_host);
+    if (rc != RT_OK) return rc;
+    for (int r = 0; r < world; ++r)
+        if (rcs[r] != RT_OK) {
+            rtamd::set_last_error("simulated rank " + std::to_string(r) + ": " + std::string(&msgs[(size_t)r * 256]));
+            return rcs[r];
+        }
+    return RT_OK;
 }
 
 // ------------------------------------------------------------- test hook
@@ -1099,7 +1396,7 @@ extern "C" int rt_test_dist_create_rccl1(rt_dist** out) {
 // collective stream is held past the rank's timeout (a peer that never
 // arrives: the wait times out and the communicator is aborted).
 extern "C" int rt_test_dist_inject(rt_dist* d, int what) {
-    if (!d || what < 0 || what > 2) return RT_ERR_INVALID_ARG;
+    if (!d || what < 0 || what > 3) return RT_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(d->mu);
     d->inject = what;
     return RT_OK;

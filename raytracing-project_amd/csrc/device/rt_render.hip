@@ -172,14 +172,20 @@ struct Workspace {
     SceneCache sc;
 };
 
+// Workspaces by (device, slot).  Slot 0 is the process's own; the simulated
+// ranks of rt_test_dist_threads run on one device concurrently, each on its
+// own host thread with its own slot (rtamd::set_workspace_slot), as separate
+// processes would hold separate workspaces.  Never deleted (frames hold
+// pointers); emptied by rt_shutdown.
 std::mutex g_ws_mu;
-std::vector<Workspace*> g_ws;   // per device; never deleted (frames hold pointers), emptied by rt_shutdown
+std::map<std::pair<int, int>, Workspace*> g_ws;
+thread_local int t_ws_slot = 0;
 
 Workspace& workspace(int dev) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    if ((int)g_ws.size() <= dev) g_ws.resize(dev + 1, nullptr);
-    if (!g_ws[dev]) g_ws[dev] = new Workspace;
-    return *g_ws[dev];
+    Workspace*& w = g_ws[{dev, t_ws_slot}];
+    if (!w) w = new Workspace;
+    return *w;
 }
 
 // One-time setup costs of this process (rt_setup_times): host wall time of
@@ -223,6 +229,7 @@ struct rt_frame {
     bool eager = false, deep = false, secondary = false, count_ops = false, fp32 = false;
     bool big = false;                          // big-stack kernels (rtdb)
     bool traced = false;
+    bool timed = false;                        // paper mode: a launch stored its waves' ticks (PaperParams::gtime)
     std::vector<int32_t> rows;
     std::vector<int32_t> rows_jrow;            // standard mode: rows | jitter row of each
     std::chrono::steady_clock::time_point t_start;
@@ -379,6 +386,16 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     std::unique_ptr<rt_frame> f(new rt_frame);
     f->ws = &workspace(dev);
     f->lock = std::unique_lock<std::mutex>(f->ws->mu);
+    // a failure below may leave uploads of this frame queued on st (some read
+    // the page-locked staging arena the next frame_begin resets): drain st
+    // before the workspace lock goes (destroyed before f)
+    struct DrainOnFail {
+        hipStream_t st;
+        bool armed = true;
+        ~DrainOnFail() {
+            if (armed) (void)hipStreamSynchronize(st);
+        }
+    } drain{st};
     Workspace& ws = *f->ws;
     const bool fp32 = (flags & RT_FLAG_FP32) != 0;
     SceneCache& sc = ws.sc;
@@ -622,6 +639,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
     }
     HIP_TRY(hipEventRecord(ws.ev[1], st));
+    drain.armed = false;
     *out = f.release();
     return RT_OK;
 }
@@ -664,6 +682,18 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
         for (int c = 0; c < f->n_tev; ++c)
             if (wait[c]) HIP_TRY(hipStreamWaitEvent(st, ws.tev[c], 0));
     }
+    // paper mode: the ext entries this call marks as its own (ext_done) are
+    // unmarked again if the call fails before its event is recorded, so that a
+    // later call never waits on an event that was not recorded
+    struct Unmark {
+        std::vector<int>& done;
+        std::vector<int32_t> marked;
+        bool keep = false;
+        ~Unmark() {
+            if (!keep)
+                for (int32_t e : marked) done[e] = 0;
+        }
+    } unmark{f->ext_done, {}};
     if (f->mode == RT_MODE_STANDARD) {
         StdParams P;
         P.W = W;
@@ -693,6 +723,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
                 const int e = f->ext_pos[rr];
                 if (e >= 0 && !f->ext_done[e]) {
                     f->ext_done[e] = f->n_tev + 1;   // (this call's index + 1)
+                    unmark.marked.push_back(e);
                     if (rr != prev_row + 1)
                         while (list.size() % 8) list.push_back(-1);
                     list.push_back(e);
@@ -740,8 +771,10 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
                 order_paper_groups(list, it == ws.paper_cost.end() ? nullptr : &it->second);
             }
             P.n_list = (int)list.size();
-            if (order_mode >= 1)
+            if (order_mode >= 1) {
                 P.gtime = ws.gtime.as<unsigned>() + (size_t)(f->list_used / 8) * paper_waves_per_group(W) * 2;
+                f->timed = true;
+            }
             f->calls.emplace_back(f->list_used, (int)f->stage.size());
             f->list_used += (int)list.size();
             f->stage.push_back(std::move(list));
@@ -769,6 +802,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
         ws.tev.push_back(e);
     }
     HIP_TRY(hipEventRecord(ws.tev[f->n_tev], st));
+    unmark.keep = true;
     f->call_st.push_back(st);
     ++f->n_tev;
     f->last_st = st;
@@ -776,9 +810,23 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
     return RT_OK;
 }
 
+int frame_end_body(rt_frame* f, rt_stats* stats);
+
 int frame_end(rt_frame* f, rt_stats* stats) {
     if (!f) { rtamd::set_last_error("rt_frame_end: frame is NULL"); return RT_ERR_INVALID_ARG; }
-    std::unique_ptr<rt_frame> own(f);
+    std::unique_ptr<rt_frame> own(f);   // (holds the workspace lock)
+    const int rc = frame_end_body(f, stats);
+    if (rc != RT_OK) {
+        // an early return left this frame's work queued: drain every stream it
+        // used before the lock goes (the next frame_begin resets the
+        // page-locked staging its copies read, and reuses its buffers)
+        (void)hipStreamSynchronize(f->st);
+        for (hipStream_t s : f->call_st) (void)hipStreamSynchronize(s);
+    }
+    return rc;
+}
+
+int frame_end_body(rt_frame* f, rt_stats* stats) {
     Workspace& ws = *f->ws;
     const hipStream_t st = f->st;
     // join the other trace streams: one wait on each one's last call (stream
@@ -801,7 +849,7 @@ int frame_end(rt_frame* f, rt_stats* stats) {
         ws.ctr_host_words = host_words;
     }
     const unsigned long long* ctr = ws.counters.as<unsigned long long>();
-    const bool timed = f->mode == RT_MODE_PAPER && !f->calls.empty() && ws.gtime.p;
+    const bool timed = f->timed;   // (some launch of this frame stored its waves' ticks)
     hipLaunchKernelGGL(k_reduce_counters, dim3(kCounterWords + (timed ? n_groups : 0)), dim3(64), 0, st, ctr, ws.ctr_host,
                        ws.gtime.as<unsigned>(), paper_waves_per_group(f->W));
     HIP_TRY(hipGetLastError());
@@ -854,10 +902,12 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
 
 }  // namespace
 
-int rtamd::release_device_workspaces() {
+void rtamd::set_workspace_slot(int slot) { t_ws_slot = slot; }
+
+int rtamd::release_device_workspaces(int min_slot) {
     int prev = 0;
     if (hipGetDevice(&prev) != hipSuccess) return RT_ERR_NO_DEVICE;
-    {
+    if (min_slot <= 0) {
         std::lock_guard<std::mutex> lk(g_fb_mu);
         if (g_fb.p) {
             (void)hipSetDevice(g_fb_dev);
@@ -865,11 +915,12 @@ int rtamd::release_device_workspaces() {
         }
     }
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    for (size_t dev = 0; dev < g_ws.size(); ++dev) {
-        Workspace* w = g_ws[dev];
-        if (!w) continue;
+    for (auto& kv : g_ws) {
+        Workspace* w = kv.second;
+        const int dev = kv.first.first;
+        if (!w || kv.first.second < min_slot) continue;
         std::lock_guard<std::mutex> wl(w->mu);   // waits for an open frame of this device
-        (void)hipSetDevice((int)dev);
+        (void)hipSetDevice(dev);
         (void)hipDeviceSynchronize();
         for (DBuf* b : {&w->nodes, &w->mats, &w->lights, &w->dlights, &w->objs, &w->ops, &w->gb, &w->ctab, &w->lrec,
                         &w->lwrec, &w->lgb, &w->fold,

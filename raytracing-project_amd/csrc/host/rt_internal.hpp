@@ -14,8 +14,12 @@ bool node_depth_ok(const rt_scene_desc& d, int idx, int level, int* maxdepth);
 // Process-unique id of a scene handle (scenes are immutable after creation,
 // so a device copy keyed by it never goes stale).
 uint64_t scene_uid(const rt_scene* s);
-// librtamd: free every per-device workspace (rt_shutdown); returns an rt_status.
-int release_device_workspaces();
+// librtamd: free every per-device workspace of slot >= min_slot (rt_shutdown:
+// all of them); returns an rt_status.
+int release_device_workspaces(int min_slot = 0);
+// librtamd: the workspace slot of the calling thread's frames (0: the
+// process's own; rt_test_dist_threads gives each simulated rank its own).
+void set_workspace_slot(int slot);
 // librtamd: rt_frame_trace of a paper-mode FP64 frame that writes one
 // paper-code byte per pixel (rtamd::paper_code_value) instead of FP64 rows:
 // the distributed frame's gather payload (rt_dist.hip).

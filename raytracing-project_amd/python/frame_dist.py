@@ -5,7 +5,15 @@ weighted round robin rotated every round, the root lighter), which balances
 cheap sky rows against expensive geometry rows.
 All ranks' row buffers are padded to the same row count so one all_gather
 collects them; rank 0 then scatters the real rows into the frame.
-Used by bench.py (RCCL, device buffers) and tests/test_dist_gloo.py (gloo).
+
+A Python TWIN of the product's partition and chunking (rt_dist.hip
+strip_owners / partition_rows / chunk_bounds; tests/test_host_lib.py pins the
+partitions equal) for CPU tests and tools only: tests/test_dist_gloo.py runs
+it over gloo with the CPU oracle as the renderer.  The product's own rank
+protocol (agreements, gathers, placement, failure verdicts) is C++ in
+rt_dist.hip dist_frame; bench.py and the CLI go through it (rt_render_dist,
+rt_render_multi), and tests/test_gpu_dist_threads.py executes it with
+concurrent ranks on one GPU.
 """
 from __future__ import annotations
 

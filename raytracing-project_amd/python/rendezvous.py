@@ -30,10 +30,16 @@ def env_ranks() -> tuple[int, int, int]:
 
 def _path(tag: str | None) -> str:
     if tag is None:
-        # the launcher's run id when it has one (torchrun: TORCHELASTIC_RUN_ID;
-        # bench.py's own spawner: RTAMD_RUN_ID), else port + the common parent
-        run = os.environ.get("RTAMD_RUN_ID") or os.environ.get("TORCHELASTIC_RUN_ID") or str(os.getppid())
-        tag = f"{os.environ.get('MASTER_PORT', '0')}_{run}"
+        # port + the common parent (the launcher's agent, or bench.py's own
+        # spawner) + the launcher's run id when it has a real one (torchrun:
+        # TORCHELASTIC_RUN_ID, which static rendezvous leaves at "none";
+        # bench.py: RTAMD_RUN_ID).  The parent pid keeps the name unique per
+        # run, so a file left by a run that died before cleanup() is never
+        # read by the next run's ranks.
+        run = os.environ.get("RTAMD_RUN_ID") or os.environ.get("TORCHELASTIC_RUN_ID") or ""
+        if run.strip().lower() in ("", "none"):
+            run = "x"
+        tag = f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{run}"
     return os.path.join(tempfile.gettempdir(), f"rtamd_uid_{tag}")
 
 

@@ -178,6 +178,8 @@ def amd_lib():
         lib.rt_dist_rows_mode.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int32)]
         lib.rt_test_render_dist_sim.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                                 _dp, C.POINTER(C.c_uint8)]
+        lib.rt_test_dist_threads.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, _dp,
+                                             C.POINTER(C.c_uint8)]
         lib.rt_dist_reduce_max.argtypes = [C.c_void_p, _dp, C.c_int]
         lib.rt_dist_barrier.argtypes = [C.c_void_p]
         lib.rt_set_device.argtypes = [C.c_int]
@@ -499,10 +501,52 @@ def dist_rows(H: int, world: int, rank: int, mode: int = RT_MODE_STANDARD) -> li
     return list(buf[:n])
 
 
+class DistRun(C.Structure):
+    """rt_test.h rt_test_dist_run."""
+    _fields_ = [("world", C.c_int), ("rgb8", C.c_int), ("frames", C.c_int), ("fault_rank", C.c_int),
+                ("fault", C.c_int), ("fault_frame", C.c_int), ("timeout_ms", C.c_int), ("msg_cap", C.c_int),
+                ("rc", C.POINTER(C.c_int)), ("ms", _dp), ("msgs", C.c_char_p)]
+
+
+FAULT_NONE, FAULT_TRACE, FAULT_SETUP, FAULT_DESC_H, FAULT_DESC_FLAGS, FAULT_ABSENT = range(6)
+RANK_ABSENT = 1
+
+
+def dist_threads(scene: Scene, width: int, height: int, mode: int, world: int, frames: int = 1,
+                 fault: int = FAULT_NONE, fault_rank: int = -1, fault_frame: int = 0, timeout_ms: int = 0,
+                 rgb8: bool = False, flags: int = RT_FLAG_NONE):
+    """rt_test_dist_threads: `frames` distributed frames with `world` ranks
+    running concurrently on the current device (one host thread, stream set
+    and workspace per rank; RCCL replaced by a same-device transport), with an
+    optional fault on one rank in one frame.  Returns (root frames
+    [frames, H, W, 3] - zeros where the root's call failed -, rc [frames,
+    world], ms [frames, world], messages [frames][world])."""
+    lib = amd_lib()
+    cap = 512
+    rc = np.zeros((frames, world), dtype=np.int32)
+    ms = np.zeros((frames, world), dtype=np.float64)
+    msgs = C.create_string_buffer(frames * world * cap)
+    out = np.zeros((frames, height, width, 3), dtype=np.uint8 if rgb8 else np.float64)
+    run = DistRun(world, 1 if rgb8 else 0, frames, fault_rank, fault, fault_frame, timeout_ms, cap,
+                  rc.ctypes.data_as(C.POINTER(C.c_int)), ms.ctypes.data_as(_dp), C.cast(msgs, C.c_char_p))
+    if rgb8:
+        r = lib.rt_test_dist_threads(scene.handle, width, height, mode, flags, C.byref(run), None,
+                                     out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    else:
+        r = lib.rt_test_dist_threads(scene.handle, width, height, mode, flags, C.byref(run),
+                                     out.ctypes.data_as(_dp), None)
+    if r != RT_OK:
+        raise RTError(r, last_error())
+    raw = msgs.raw
+    text = [[raw[(f * world + k) * cap:(f * world + k + 1) * cap].split(b"\0", 1)[0].decode("utf-8", "replace")
+             for k in range(world)] for f in range(frames)]
+    return out, rc, ms, text
+
+
 def render_dist_sim(scene: Scene, width: int, height: int, mode: int, world: int, rgb8: bool = False,
                     flags: int = RT_FLAG_NONE) -> np.ndarray:
-    """rt_test_render_dist_sim: the multi-GPU frame path with `world` ranks
-    simulated on the current device (RCCL gather replaced by copies)."""
+    """rt_test_render_dist_sim: one distributed frame with `world` ranks
+    running concurrently on the current device (rt_test_dist_threads)."""
     lib = amd_lib()
     if rgb8:
         out = np.zeros((height, width, 3), dtype=np.uint8)

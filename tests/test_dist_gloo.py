@@ -2,12 +2,16 @@
 
 Each rank renders its interleaved row strips (standard mode: every strip
 starts its own mt19937 stream offset; paper mode: neighbour rows outside the
-strip are re-traced), the padded row buffers go through frame_dist.DistFrame — the same chunked
-gather-to-rank-0 pipeline bench.py runs over RCCL — and rank 0 scatters
-them into the frame.  The
-per-rank renderer here is the CPU oracle (test infrastructure), so this test
-pins the partition / offset / gather / scatter logic, not the GPU kernels
-(tests/test_gpu_jitter_rows.py covers rt_render_rows_device on the GPU)."""
+strip are re-traced), the padded row buffers go through frame_dist.DistFrame
+- a Python twin of the product's partition and chunked gather-to-rank-0
+layout (rt_dist.hip; tests/test_host_lib.py pins the partitions equal) - and
+rank 0 scatters them into the frame.  The per-rank renderer here is the CPU
+oracle (test infrastructure), so this test pins the partition / stream
+offsets / gather / scatter LOGIC over a real two-process torch.distributed
+group; it does not run the product's C++ rank protocol (dist_frame: frame
+agreements, RCCL gathers, placement, failure verdicts), which
+tests/test_gpu_dist_threads.py executes with concurrent ranks on one GPU, nor
+the GPU kernels (tests/test_gpu_jitter_rows.py)."""
 import os
 import socket
 
