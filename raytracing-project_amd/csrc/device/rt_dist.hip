@@ -145,27 +145,12 @@ std::vector<std::vector<int32_t>> partition_rows(int H, int world, int mode, int
     return rows;
 }
 
-// `chunks` contiguous pieces of [0, m), each a whole number of strips of S
-// rows (a chunk never splits a strip, so a paper-mode strip's rows and halo
-// are traced by one launch), of decreasing size: weights chunks, chunks-1,
-// ..., 1 (4 chunks: 40/30/20/10 %).  Chunk k is gathered while chunk k+1 is
-// traced, so only the last, smallest chunk's gather is exposed.
-std::vector<std::pair<int, int>> chunk_bounds(int m, int chunks, int S = 1) {
-    const int64_t units = (m + S - 1) / S;
-    chunks = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, units));
-    const int64_t wsum = (int64_t)chunks * (chunks + 1) / 2;
-    std::vector<std::pair<int, int>> out;
-    int64_t acc = 0;
-    for (int k = 0; k < chunks; ++k) {
-        const int64_t u0 = acc * units / wsum;
-        acc += chunks - k;
-        const int64_t u1 = acc * units / wsum;
-        const int a = (int)std::min<int64_t>(m, u0 * S), b = (int)std::min<int64_t>(m, u1 * S);
-        if (b > a) out.emplace_back(a, b);
-    }
-    if (out.empty()) out.emplace_back(0, 0);
-    return out;
-}
+// Row chunks of a rank's share: rtamd::row_chunks (rt_render.hip), whole
+// strips of S rows (a chunk never splits a strip, so a paper-mode strip's
+// rows and halo are traced by one launch), of decreasing size (4 chunks:
+// 40/30/20/10 %).  Chunk k is gathered while chunk k+1 is traced, so only the
+// last, smallest chunk's gather is exposed.
+std::vector<std::pair<int, int>> chunk_bounds(int m, int chunks, int S = 1) { return rtamd::row_chunks(m, chunks, S); }
 
 // Gathered slot i (row_bytes bytes) -> row rows[i] of dst; rows[i] < 0 is padding.
 template <class V>
@@ -621,7 +606,11 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     // per pixel, 1 B/px crosses xGMI, and the root decodes (k_place_codes)
     const bool codes = coll && mode == RT_MODE_PAPER && !(flags & RT_FLAG_FP32);
     const size_t row_bytes = codes ? (size_t)Wc : row_elems * (kind ? 1 : sizeof(double));   // gathered per row
-    const auto bounds = chunk_bounds(m, coll ? frame_chunks(mode) : 1, S);
+    // (one GPU: paper frames in chunks too, so that each chunk's finish pass
+    // overlaps the next chunk's primary on the other stream)
+    // (kChunks bounds the per-chunk event arrays)
+    const auto bounds = chunk_bounds(
+        m, std::min(kChunks, coll ? frame_chunks(mode) : (mode == RT_MODE_PAPER ? rtamd::paper_chunks_1gpu() : 1)), S);
     const bool direct = !coll && kind == 0;   // trace straight into the caller's frame
     DevBuf& stage = D.sim_stage ? *D.sim_stage : D.stage;
     auto fail = [&](int code, const char* what) {
@@ -725,7 +714,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             rc = codes ? rtamd::frame_trace_paper_codes(f, a, hi, D.mine.as<uint8_t>() + (size_t)a * row_bytes, cst)
                        : rt_frame_trace(f, a, hi, fb_rows + (size_t)a * row_elems, cst);
         if (rc == RT_OK && kind == 1 && hi > a && !codes) {
-            uint8_t* dst8 = coll ? D.mine8.as<uint8_t>() + (size_t)a * row_elems : static_cast<uint8_t*>(out_root);
+            // (one GPU: rows are the frame's, in order, so chunk rows land at their own place)
+            uint8_t* dst8 = (coll ? D.mine8.as<uint8_t>() : static_cast<uint8_t*>(out_root)) + (size_t)a * row_elems;
             if (hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) fail(RT_ERR_HIP, "event record failed");
             if (rc == RT_OK) rc = rt_framebuffer_to_rgb8_device(fb_rows + (size_t)a * row_elems, (size_t)(hi - a) * W, dst8, cst);
             if (rc == RT_OK && hipEventRecord(D.ev_tb[n_tb++], cst) != hipSuccess) fail(RT_ERR_HIP, "event record failed");

@@ -169,6 +169,8 @@ struct Workspace {
     std::vector<rtamd::JRange> jranges;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
+    std::vector<hipEvent_t> pev;   // paper mode: the end of each call's primary pass (pool)
+    hipStream_t aux_st = nullptr;  // render_rows_impl: a paper frame's odd chunks
     SceneCache sc;
 };
 
@@ -659,15 +661,18 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
     const hipStream_t st = hs ? hs : f->st;
     const int W = f->W, n = ri1 - ri0;
     unsigned long long* ctr = ws.counters.as<unsigned long long>();
-    // another stream first waits for the scene upload and jitter (begin); in
-    // paper mode a chunk that reads primary hits an earlier call computed on
-    // another stream waits for that call (adjacent strips share a neighbour
-    // row: one rank's whole frame; a rank of a split frame traces strips that
-    // share none, so its chunks overlap on the two streams)
+    // another stream first waits for the scene upload and jitter (begin).  In
+    // paper mode a chunk whose finish pass reads primary hits that an earlier
+    // call computed on another stream waits for that call's PRIMARY pass
+    // (adjacent strips share a neighbour row: one GPU's chunked frame, or
+    // adjacent strips of one rank), and only its finish waits: its primary
+    // computes new entries only, so it overlaps the earlier call's finish
+    // (latency-bound) on the other stream.
     const auto t_launch = SClock::now();
     if (st != f->st) HIP_TRY(hipStreamWaitEvent(st, ws.ev[1], 0));
+    std::vector<char> wait;
     if (f->mode == RT_MODE_PAPER && f->n_tev > 0) {
-        std::vector<char> wait(f->n_tev, 0);
+        wait.assign(f->n_tev, 0);
         for (int i = ri0; i < ri1; ++i) {
             const int r = f->rows[i];
             for (int rr = r - 1; rr <= r + 1; ++rr) {
@@ -679,8 +684,6 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
                 }
             }
         }
-        for (int c = 0; c < f->n_tev; ++c)
-            if (wait[c]) HIP_TRY(hipStreamWaitEvent(st, ws.tev[c], 0));
     }
     // paper mode: the ext entries this call marks as its own (ext_done) are
     // unmarked again if the call fails before its event is recorded, so that a
@@ -786,6 +789,14 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
             else rtd::launch_paper(f->eager, f->deep, f->count_ops, g1, st, f->S, P);
             HIP_TRY(hipGetLastError());
         }
+        if ((int)ws.pev.size() <= f->n_tev) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ws.pev.push_back(e);
+        }
+        HIP_TRY(hipEventRecord(ws.pev[f->n_tev], st));
+        for (size_t c = 0; c < wait.size(); ++c)
+            if (wait[c]) HIP_TRY(hipStreamWaitEvent(st, ws.pev[c], 0));
         dim3 g2((W + 63) / 64, (n + 3) / 4);
         if (f->fp32) rtf::launch_paper_finish(g2, st, P);
         else rtd::launch_paper_finish(g2, st, P);
@@ -895,7 +906,19 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
     rt_frame* f = nullptr;
     int rc = frame_begin(s, W, H, mode, flags, rows_host, n_rows, st, &f);
     if (rc != RT_OK) return rc;
-    rc = frame_trace(f, 0, n_rows, fb_dev, nullptr);
+    // paper mode: row chunks alternating between a second stream and the
+    // frame's (rtamd::row_chunks), so that each chunk's finish overlaps the
+    // next chunk's primary; the last chunk runs on the frame stream
+    std::vector<std::pair<int, int>> bounds{{0, n_rows}};
+    if (mode == RT_MODE_PAPER && rtamd::paper_chunks_1gpu() > 1) {
+        Workspace& ws = *f->ws;
+        if (!ws.aux_st && hipStreamCreateWithFlags(&ws.aux_st, hipStreamNonBlocking) != hipSuccess) ws.aux_st = nullptr;
+        if (ws.aux_st) bounds = rtamd::row_chunks(n_rows, rtamd::paper_chunks_1gpu(), RT_PAPER_STRIP_ROWS);
+    }
+    for (size_t k = 0; k < bounds.size() && rc == RT_OK; ++k) {
+        const hipStream_t cst = ((bounds.size() - 1 - k) & 1) ? f->ws->aux_st : nullptr;
+        rc = frame_trace(f, bounds[k].first, bounds[k].second, fb_dev + (size_t)bounds[k].first * W * 3, cst);
+    }
     const int rc2 = frame_end(f, stats);
     return rc != RT_OK ? rc : rc2;
 }
@@ -903,6 +926,38 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
 }  // namespace
 
 void rtamd::set_workspace_slot(int slot) { t_ws_slot = slot; }
+
+// Row chunks of a frame or a rank's share (see rt_internal.hpp).
+std::vector<std::pair<int, int>> rtamd::row_chunks(int m, int chunks, int S) {
+    const int64_t units = (m + S - 1) / S;
+    chunks = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, units));
+    const int64_t wsum = (int64_t)chunks * (chunks + 1) / 2;
+    std::vector<std::pair<int, int>> out;
+    int64_t acc = 0;
+    for (int k = 0; k < chunks; ++k) {
+        const int64_t u0 = acc * units / wsum;
+        acc += chunks - k;
+        const int64_t u1 = acc * units / wsum;
+        const int a = (int)std::min<int64_t>(m, u0 * S), b = (int)std::min<int64_t>(m, u1 * S);
+        if (b > a) out.emplace_back(a, b);
+    }
+    if (out.empty()) out.emplace_back(0, 0);
+    return out;
+}
+
+// RT_PAPER_CHUNKS_1GPU (measurement A/B; 1 .. 4, default 1): row chunks of a
+// paper frame rendered by one GPU, alternating between two streams so that
+// chunk k's finish pass overlaps chunk k+1's primary.  Measured on config 5
+// (profiles/r05_ab/ab_paper_chunks_1gpu.txt): 1 chunk 5.34 ms, 2 chunks 5.37,
+// 4 chunks 5.57 - the chunks' own tails and their separate costliest-first
+// orders cost more than the overlapped finish saves - so one launch pair.
+int rtamd::paper_chunks_1gpu() {
+    static const int c = [] {
+        const char* e = std::getenv("RT_PAPER_CHUNKS_1GPU");
+        return e && *e ? std::max(1, std::min(4, std::atoi(e))) : 1;
+    }();
+    return c;
+}
 
 int rtamd::release_device_workspaces(int min_slot) {
     int prev = 0;
@@ -941,6 +996,11 @@ int rtamd::release_device_workspaces(int min_slot) {
         for (auto& e : w->tev)
             if (e) (void)hipEventDestroy(e);
         w->tev.clear();
+        for (auto& e : w->pev)
+            if (e) (void)hipEventDestroy(e);
+        w->pev.clear();
+        if (w->aux_st) (void)hipStreamDestroy(w->aux_st);
+        w->aux_st = nullptr;
         w->sc = SceneCache();
     }
     (void)hipSetDevice(prev);

@@ -3,6 +3,8 @@
 
 #include <cstdint>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "rt.h"
 
@@ -17,6 +19,12 @@ uint64_t scene_uid(const rt_scene* s);
 // librtamd: free every per-device workspace of slot >= min_slot (rt_shutdown:
 // all of them); returns an rt_status.
 int release_device_workspaces(int min_slot = 0);
+// librtamd: `chunks` contiguous pieces of [0, m), each a whole number of
+// strips of S rows, of decreasing size (weights chunks, chunks-1, ..., 1:
+// 4 chunks = 40/30/20/10 %).
+std::vector<std::pair<int, int>> row_chunks(int m, int chunks, int S = 1);
+// librtamd: row chunks of a one-GPU paper frame (RT_PAPER_CHUNKS_1GPU, default 4).
+int paper_chunks_1gpu();
 // librtamd: the workspace slot of the calling thread's frames (0: the
 // process's own; rt_test_dist_threads gives each simulated rank its own).
 void set_workspace_slot(int slot);
