@@ -380,7 +380,9 @@ int rt_host_unregister(void* host);
  * out[0] scene compile + upload (first frame of each scene), out[1] jitter
  * checkpoint-table builds / extensions, out[2] first trace-kernel launch
  * (loads the kernels' code object onto the device), out[3] first jitter-fill
- * launch (its code object).  n <= 4 entries are written. */
+ * launch (its code object), out[4] device allocations (hipMalloc), out[5]
+ * page-locked host allocations, out[6] stream / event creation.  n <= 7
+ * entries are written. */
 int rt_setup_times(double* out, int n);
 /* Release every device resource the library caches (per-device workspaces,
  * resident scenes and jitter tables, the rt_render_multi device groups with

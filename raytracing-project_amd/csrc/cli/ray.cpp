@@ -94,6 +94,7 @@ int main(int argc, char** argv) {
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";
     const auto t0 = std::chrono::steady_clock::now();
     prefault.join();
+    const auto t_joined = std::chrono::steady_clock::now();
     try {
         tracer.render_rgb8(rgb);
     } catch (const std::exception& e) {
@@ -109,7 +110,10 @@ int main(int argc, char** argv) {
     }
     const auto t2 = std::chrono::steady_clock::now();
     teardown.done = true;
-    (void)rt_shutdown();
+    // With one GPU the library holds no communicators: its device memory is
+    // the process's and goes with it at the _Exit below.  Several GPUs:
+    // destroy the RCCL communicators first.
+    if (n_gpus != 1) (void)rt_shutdown();
     const auto t3 = std::chrono::steady_clock::now();
     std::string mode_str = paper_mode ? " (paper mode)" : "";
     std::cout << "Wrote " << out_path << " (" << W << "x" << H << ")" << mode_str << "\n";
@@ -118,12 +122,20 @@ int main(int argc, char** argv) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const double ms_render = ms(t0, t1);
         const double rays = (double)(s.rays_intersect + s.rays_occluded);
-        double setup[4] = {0, 0, 0, 0};
-        (void)rt_setup_times(setup, 4);
+        double setup[11] = {};
+        (void)rt_setup_times(setup, 11);
+        // ms_render's host split, in order: output-buffer prefault join,
+        // rt_render_rgb8's group setup, rt_frame_begin (scene compile + upload,
+        // jitter checkpoint table, jitter launch), the trace launches,
+        // rt_frame_end (waits for the device), the D2H copy
         std::printf(
             "{\"ms_hip_init\": %.3f, \"ms_setup_scene\": %.3f, \"ms_setup_jtable\": %.3f, "
-            "\"ms_setup_trace_load\": %.3f, \"ms_setup_jitter_load\": %.3f, \"ms_shutdown\": %.3f}\n",
-            ms(t_hip0, t_hip1), setup[0], setup[1], setup[2], setup[3], ms(t2, t3));
+            "\"ms_setup_trace_load\": %.3f, \"ms_setup_jitter_load\": %.3f, \"ms_setup_alloc\": %.3f, "
+            "\"ms_setup_pinned\": %.3f, \"ms_setup_streams\": %.3f, \"ms_prefault_join\": %.3f, "
+            "\"ms_group\": %.3f, \"ms_frame_begin\": %.3f, \"ms_frame_trace\": %.3f, \"ms_frame_end\": %.3f, "
+            "\"ms_shutdown\": %.3f}\n",
+            ms(t_hip0, t_hip1), setup[0], setup[1], setup[2], setup[3], setup[4], setup[5], setup[6],
+            ms(t0, t_joined), setup[10], setup[7], setup[8], setup[9], ms(t2, t3));
         std::printf(
             "{\"rays_intersect\": %llu, \"rays_occluded\": %llu, \"rays_traced\": %llu, \"n_gpus\": %d, "
             "\"ms_load\": %.3f, \"ms_rng\": %.3f, \"ms_kernel\": %.3f, \"ms_gather\": %.3f, \"ms_tobyte\": %.3f, "

@@ -20,6 +20,8 @@
 #include <utility>
 #include <vector>
 
+#include "rt_internal.hpp"
+
 namespace rtamd {
 
 struct PinnedArena {
@@ -41,6 +43,7 @@ struct PinnedArena {
             cap = std::max<size_t>({2 * cap, need, (size_t)1 << 16});
             p = nullptr;
             used = 0;
+            SetupTimer tm(kSetupPinned);
             if (hipHostMalloc(reinterpret_cast<void**>(&p), cap, hipHostMallocDefault) != hipSuccess) {
                 p = nullptr;
                 cap = 0;

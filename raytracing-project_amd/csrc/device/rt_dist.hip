@@ -74,6 +74,7 @@ struct DevBuf {
         p = nullptr;
         n = 0;
         const size_t want = bytes + bytes / 16 + 256;
+        rtamd::SetupTimer tm(rtamd::kSetupAlloc);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) n = want;
         return e;
@@ -135,14 +136,51 @@ std::vector<int> strip_owners(int n_strips, int world, int mode, int kind) {
 }
 
 // Output rows of every rank (ascending per rank), strips of strip_height(mode).
+// (A partition balanced on measured strip costs - the strips' summed primary
+// wave ticks, exchanged in the trace-status agreement, longest processing
+// time first - was measured and rejected: slower at 2 ranks, no better at 4
+// and 8, profiles/r05_ab/ab_cost_partition.txt.)
 std::vector<std::vector<int32_t>> partition_rows(int H, int world, int mode, int kind) {
     const int S = strip_height(mode);
     const int n_strips = (H + S - 1) / S;
-    const std::vector<int> own = strip_owners(n_strips, world, mode, kind);
     std::vector<std::vector<int32_t>> rows((size_t)world);
+    const std::vector<int> own = strip_owners(n_strips, world, mode, kind);
     for (int st = 0; st < n_strips; ++st)
         for (int r = st * S; r < std::min(H, (st + 1) * S); ++r) rows[own[st]].push_back(r);
     return rows;
+}
+
+uint64_t fnv_bytes(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+// Content hash of a scene (the IR arrays and camera fields; no padding bytes),
+// equal on every rank that loaded the same JSON: part of the frame descriptor
+// the ranks check, and of the key their strip costs belong to.
+int64_t scene_hash(const rt_scene* s) {
+    if (!s) return 0;
+    const rt_scene_desc& d = *rt_scene_get_desc(s);
+    uint64_t h = 1469598103934665603ull;
+    h = fnv_bytes(h, d.camera.eye, sizeof d.camera.eye);
+    h = fnv_bytes(h, d.camera.P, sizeof d.camera.P);
+    h = fnv_bytes(h, &d.camera.Lx, sizeof(double));
+    h = fnv_bytes(h, &d.camera.Ly, sizeof(double));
+    h = fnv_bytes(h, &d.camera.dpi, sizeof(int32_t));
+    h = fnv_bytes(h, d.background, sizeof d.background);
+    h = fnv_bytes(h, d.ambient, sizeof d.ambient);
+    h = fnv_bytes(h, &d.medium_index, sizeof(double));
+    h = fnv_bytes(h, &d.recursion_limit, sizeof(int32_t));
+    h = fnv_bytes(h, d.lights, sizeof(rt_light) * (size_t)d.n_lights);
+    h = fnv_bytes(h, d.materials, sizeof(rt_material) * (size_t)d.n_materials);
+    h = fnv_bytes(h, d.nodes, sizeof(rt_node) * (size_t)d.n_nodes);
+    h = fnv_bytes(h, d.objects, sizeof(int32_t) * (size_t)d.n_objects);
+    h = fnv_bytes(h, d.dir_lights, sizeof(rt_dir_light) * (size_t)d.n_dir_lights);
+    return (int64_t)(h >> 2);   // (62 bits: v and -v both representable)
 }
 
 // Row chunks of a rank's share: rtamd::row_chunks (rt_render.hip), whole
@@ -325,6 +363,7 @@ struct rt_dist {
     std::vector<int32_t> rowtab_host;          // source of the async row-table upload
     std::mutex mu;                            // one frame at a time per rank
     DevBuf* sim_stage = nullptr;              // rt_test_dist_sim_rank: shared stage, copies instead of RCCL
+    size_t xchg_cap = 0;                      // int64 slots of xchg / xchg_host
     SimGroup* simg = nullptr;                 // rt_test_dist_threads: concurrent ranks, same-device transport
     DevBuf simtmp;                            //   its all-reduce temporary
     bool force_collective = false;            // rt_test_dist_create_rccl1: world 1 through ncclGather
@@ -342,23 +381,33 @@ struct rt_dist {
     std::atomic<double> abort_ms{-1.0};       //   its duration once done
     double timeout_ms = 120000.0;             // RT_DIST_TIMEOUT_MS / rt_dist_set_timeout
     int inject = 0;                           // rt_test_dist_inject (next frame only)
+    std::map<const rt_scene*, int64_t> scene_hashes;   // (scenes are immutable)
     bool collective() const { return world > 1 || force_collective; }
 };
 
 namespace {
 
-int dist_init_streams(rt_dist& D) {
-    if (D.comm_st) return RT_OK;
-    int lo = 0, hi = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIP_TRY(hipStreamCreateWithPriority(&D.comm_st, hipStreamNonBlocking, hi));
-    HIP_TRY(hipStreamCreateWithFlags(&D.alt_st, hipStreamNonBlocking));
-    for (auto& e : D.ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto& e : D.ev_tb) HIP_TRY(hipEventCreate(&e));
-    for (auto& e : D.ev_gs) HIP_TRY(hipEventCreate(&e));
-    for (auto& e : D.ev_ge) HIP_TRY(hipEventCreate(&e));
-    HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&D.ev_desc, hipEventDisableTiming));
+// A rank's streams and events, created on first need: the collective stream
+// only for collective frames, the alternate chunk stream only for frames of
+// more than one chunk (a one-GPU frame of the `ray` CLI creates neither: the
+// first stream creations of a process cost ~30 ms of setup,
+// profiles/r05_cli_split.txt).
+int dist_init_streams(rt_dist& D, bool coll, bool alt) {
+    rtamd::SetupTimer tm(rtamd::kSetupStreams);
+    if (!D.ev_alt) {
+        for (auto& e : D.ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& e : D.ev_tb) HIP_TRY(hipEventCreate(&e));
+        for (auto& e : D.ev_gs) HIP_TRY(hipEventCreate(&e));
+        for (auto& e : D.ev_ge) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&D.ev_desc, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
+    }
+    if (coll && !D.comm_st) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&D.comm_st, hipStreamNonBlocking, hi));
+    }
+    if (alt && !D.alt_st) HIP_TRY(hipStreamCreateWithFlags(&D.alt_st, hipStreamNonBlocking));
     return RT_OK;
 }
 
@@ -378,15 +427,26 @@ int dist_init_streams(rt_dist& D) {
 // asynchronous error; on either the communicator is aborted (ncclCommAbort)
 // and the handle refuses further frames: a rank whose peer died returns
 // RT_ERR_HIP instead of hanging.
-constexpr int kDescFields = 5;
-size_t xchg_slots(int world) { return 2 * kDescFields + 2 * (size_t)world; }
+// Descriptor: W, H, mode, output kind, flags and the scene's content hash
+// (ranks that loaded different scenes refuse the frame together).
+constexpr int kDescFields = 6;
 
-int dist_init_xchg(rt_dist& D) {
-    const size_t bytes = xchg_slots(D.world) * sizeof(int64_t);
+// slots: the agreement 1 descriptor (v, -v) + setup status per rank, then the
+// trace status per rank
+int dist_init_xchg(rt_dist& D, size_t slots) {
+    if (slots <= D.xchg_cap && D.xchg_host) return RT_OK;
+    const size_t bytes = slots * sizeof(int64_t);
     HIP_TRY(D.xchg.ensure(bytes));
-    if (!D.xchg_host) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&D.xchg_host), bytes, hipHostMallocDefault));
+    if (D.xchg_host) (void)hipHostFree(D.xchg_host);   // (the previous frame's readbacks are done)
+    D.xchg_host = nullptr;
+    D.xchg_cap = 0;
+    rtamd::SetupTimer tm(rtamd::kSetupPinned);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&D.xchg_host), bytes, hipHostMallocDefault));
+    D.xchg_cap = slots;
     return RT_OK;
 }
+
+
 
 // The communicator is aborted on a helper thread: ncclCommAbort can wait
 // for work already queued on the collective stream (a held stream kept it
@@ -587,15 +647,27 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     else if (root && !out_root) { rtamd::set_last_error("rt_render_dist: the root needs an output buffer"); rc = RT_ERR_INVALID_ARG; }
     if (rc != RT_OK && !coll) return rc;
     {
-        const int rs = dist_init_streams(D);   // the collective stream itself: without it nothing can be joined
+        // (the collective stream itself: without it nothing can be joined)
+        const int rs = dist_init_streams(D, coll, coll || (mode == RT_MODE_PAPER && rtamd::paper_chunks_1gpu() > 1));
         if (rs != RT_OK) return rs;
-    }
-    if (coll) {
-        const int rx = dist_init_xchg(D);
-        if (rx != RT_OK) return rx;
     }
     const int Wc = std::max(W, 1), Hc = std::max(H, 1);
     const int S = strip_height(mode == RT_MODE_PAPER ? RT_MODE_PAPER : RT_MODE_STANDARD);
+    int64_t shash = 0;   // (the scene's content hash, checked with the descriptor)
+    if (s) {
+        auto it = D.scene_hashes.find(s);
+        if (it == D.scene_hashes.end()) {
+            if (D.scene_hashes.size() > 64) D.scene_hashes.clear();
+            it = D.scene_hashes.emplace(s, scene_hash(s)).first;
+        }
+        shash = it->second;
+    }
+    const size_t n_desc = 2 * kDescFields + (size_t)D.world;
+    const size_t n_stat = (size_t)D.world;
+    if (coll) {
+        const int rx = dist_init_xchg(D, n_desc + n_stat);
+        if (rx != RT_OK) return rx;
+    }
     const std::vector<std::vector<int32_t>> part = partition_rows(Hc, D.world, mode, kind);
     const std::vector<int32_t>& rows = part[D.rank];
     const int n = (int)rows.size();
@@ -657,10 +729,9 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     // too.
     int64_t* xd = D.xchg.as<int64_t>();
     int64_t* xh = D.xchg_host;
-    const size_t n_desc = 2 * kDescFields + (size_t)D.world;
     bool agreed = !coll;
     auto issue_agreement = [&]() -> bool {
-        const int64_t v[kDescFields] = {W, H, mode, kind, flags};
+        const int64_t v[kDescFields] = {W, H, mode, kind, flags, shash};
         for (int i = 0; i < kDescFields; ++i) {
             xh[i] = v[i];
             xh[kDescFields + i] = -v[i];
@@ -699,7 +770,6 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     double* fb_rows = direct ? static_cast<double*>(out_root) : D.mine.as<double>();
     int n_tb = 0, n_g = 0;
     bool status_sent = false;
-    const size_t n_stat = (size_t)D.world;
     for (size_t k = 0; k < bounds.size(); ++k) {
         const int a = bounds[k].first, b = bounds[k].second, hi = std::min(b, n);
         // chunks alternate between two streams, the last one on st: the frame's
@@ -734,7 +804,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             }
             std::string bad;
             for (int i = 0; i < kDescFields; ++i) {
-                static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags"};
+                static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags", "scene"};
                 if (xh[i] != -xh[kDescFields + i]) bad += std::string(bad.empty() ? "" : ", ") + names[i];
             }
             std::string failed;
@@ -796,7 +866,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     }
     // alt_st's last work (a chunk's toByte) into st, which rt_frame_end
     // synchronises (without toByte, rt_frame_end joins alt_st's last trace call)
-    if (n_tb > 0 && (hipEventRecord(D.ev_alt, D.alt_st) != hipSuccess || hipStreamWaitEvent(st, D.ev_alt, 0) != hipSuccess))
+    if (n_tb > 0 && D.alt_st &&
+        (hipEventRecord(D.ev_alt, D.alt_st) != hipSuccess || hipStreamWaitEvent(st, D.ev_alt, 0) != hipSuccess))
         fail(RT_ERR_HIP, "stream join failed");
     const int rc_end = f ? rt_frame_end(f, stats) : RT_OK;   // joins and synchronises the trace streams
     if (coll) {
@@ -984,6 +1055,8 @@ int render_multi(const rt_scene* s, int W, int H, int mode, int flags, int n_gpu
     HIP_TRY(hipSetDevice(0));
     DevBuf& out = kind ? G->out8 : G->out;
     HIP_TRY(out.ensure(out_bytes));
+    rtamd::note_setup_ms(rtamd::kLastGroup,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     std::vector<rt_stats> st(n);
     std::vector<int> rcs(n, RT_OK);
     std::vector<std::string> errs(n);
@@ -1284,7 +1357,7 @@ extern "C" int rt_test_dist_sim_rank(const rt_scene* s, int W, int H, int mode, 
         d->rank = rank;
         d->sim_stage = &stage;
         HIP_TRY(hipGetDevice(&d->device));
-        const int rs = dist_init_streams(streams);
+        const int rs = dist_init_streams(streams, true, true);
         if (rs != RT_OK) return rs;
         d->comm_st = streams.comm_st;
         d->alt_st = streams.alt_st;
@@ -1314,7 +1387,7 @@ extern "C" int rt_dist_reduce_max(rt_dist* d, double* vals_host, int n) {
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(d->device));
-    int rc = dist_init_streams(*d);
+    int rc = dist_init_streams(*d, true, false);
     if (rc == RT_OK) {
         const size_t bytes = (size_t)n * sizeof(double);
         if (d->red.ensure(bytes) != hipSuccess ||

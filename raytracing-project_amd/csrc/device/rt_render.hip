@@ -113,6 +113,7 @@ struct DBuf {
         p = nullptr;
         n = 0;
         size_t want = bytes + bytes / 8 + 256;
+        rtamd::SetupTimer tm(rtamd::kSetupAlloc);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) n = want;
         return e;
@@ -197,6 +198,7 @@ Workspace& workspace(int dev) {
 struct SetupTimes {
     std::mutex mu;
     double scene_ms = 0.0, jtable_ms = 0.0, trace_launch_ms = 0.0, jitter_launch_ms = 0.0;
+    double extra[rtamd::kSetupSlots] = {};   // rtamd::note_setup_ms slots (4..)
     bool trace_launched = false, jitter_launched = false;
 };
 SetupTimes g_setup;
@@ -491,8 +493,10 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     f->big = big;
     f->rows.assign(rows_host, rows_host + n_rows);
     f->t_start = t_start;
-    if (!ws.ev[0])
+    if (!ws.ev[0]) {
+        rtamd::SetupTimer tm(rtamd::kSetupStreams);
         for (int i = 0; i < 4; ++i) HIP_TRY(hipEventCreate(&ws.ev[i]));
+    }
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
@@ -643,6 +647,11 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     HIP_TRY(hipEventRecord(ws.ev[1], st));
     drain.armed = false;
     *out = f.release();
+    rtamd::note_setup_ms(rtamd::kLastBegin, ms_since(t_start));
+    {
+        std::lock_guard<std::mutex> lk(g_setup.mu);
+        g_setup.extra[rtamd::kLastTrace] = 0.0;   // (this frame's trace calls add to it)
+    }
     return RT_OK;
 }
 
@@ -813,6 +822,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
         ws.tev.push_back(e);
     }
     HIP_TRY(hipEventRecord(ws.tev[f->n_tev], st));
+    rtamd::note_setup_ms(rtamd::kLastTrace, ms_since(t_launch));
     unmark.keep = true;
     f->call_st.push_back(st);
     ++f->n_tev;
@@ -826,7 +836,9 @@ int frame_end_body(rt_frame* f, rt_stats* stats);
 int frame_end(rt_frame* f, rt_stats* stats) {
     if (!f) { rtamd::set_last_error("rt_frame_end: frame is NULL"); return RT_ERR_INVALID_ARG; }
     std::unique_ptr<rt_frame> own(f);   // (holds the workspace lock)
+    const auto t_end = SClock::now();
     const int rc = frame_end_body(f, stats);
+    rtamd::note_setup_ms(rtamd::kLastEnd, ms_since(t_end));
     if (rc != RT_OK) {
         // an early return left this frame's work queued: drain every stream it
         // used before the lock goes (the next frame_begin resets the
@@ -855,6 +867,7 @@ int frame_end_body(rt_frame* f, rt_stats* stats) {
         if (ws.ctr_host) (void)hipHostFree(ws.ctr_host);   // (the previous frame's readback is done)
         ws.ctr_host = nullptr;
         ws.ctr_host_words = 0;
+        rtamd::SetupTimer tm(rtamd::kSetupPinned);
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ws.ctr_host), host_words * sizeof(unsigned long long),
                               hipHostMallocDefault));
         ws.ctr_host_words = host_words;
@@ -926,6 +939,13 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
 }  // namespace
 
 void rtamd::set_workspace_slot(int slot) { t_ws_slot = slot; }
+
+void rtamd::note_setup_ms(int slot, double ms) {
+    if (slot < 4 || slot >= kSetupSlots) return;
+    std::lock_guard<std::mutex> lk(g_setup.mu);
+    if (slot < kLastBegin || slot == kLastTrace) g_setup.extra[slot] += ms;
+    else g_setup.extra[slot] = ms;
+}
 
 // Row chunks of a frame or a rank's share (see rt_internal.hpp).
 std::vector<std::pair<int, int>> rtamd::row_chunks(int m, int chunks, int S) {
@@ -1018,7 +1038,7 @@ extern "C" int rt_setup_times(double* out, int n) {
     if (!out || n < 0) return RT_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(g_setup.mu);
     const double v[4] = {g_setup.scene_ms, g_setup.jtable_ms, g_setup.trace_launch_ms, g_setup.jitter_launch_ms};
-    for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+    for (int i = 0; i < n && i < rtamd::kSetupSlots; ++i) out[i] = i < 4 ? v[i] : g_setup.extra[i];
     return RT_OK;
 }
 

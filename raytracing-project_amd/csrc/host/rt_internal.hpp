@@ -1,6 +1,7 @@
 // rt_internal.hpp — helpers shared between librt_host and librtamd.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <utility>
@@ -25,6 +26,25 @@ int release_device_workspaces(int min_slot = 0);
 std::vector<std::pair<int, int>> row_chunks(int m, int chunks, int S = 1);
 // librtamd: row chunks of a one-GPU paper frame (RT_PAPER_CHUNKS_1GPU, default 4).
 int paper_chunks_1gpu();
+// librtamd: host costs reported by rt_setup_times.  Slots 4..6 accumulate
+// over the process (device allocations, page-locked allocations, stream /
+// event creation; scope timers around those calls); slots 7..10 hold the last
+// frame's host split (rt_frame_begin, the rt_frame_trace calls, rt_frame_end
+// including its wait for the device, and rt_render_multi's own setup before
+// its frame: device group, output buffer).
+enum {
+    kSetupAlloc = 4, kSetupPinned = 5, kSetupStreams = 6,
+    kLastBegin = 7, kLastTrace = 8, kLastEnd = 9, kLastGroup = 10, kSetupSlots = 11
+};
+void note_setup_ms(int slot, double ms);   // slots 4..6: add; 7..10: set (kLastTrace adds within a frame)
+struct SetupTimer {
+    int slot;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit SetupTimer(int s) : slot(s) {}
+    ~SetupTimer() {
+        note_setup_ms(slot, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
 // librtamd: the workspace slot of the calling thread's frames (0: the
 // process's own; rt_test_dist_threads gives each simulated rank its own).
 void set_workspace_slot(int slot);
@@ -32,4 +52,5 @@ void set_workspace_slot(int slot);
 // paper-code byte per pixel (rtamd::paper_code_value) instead of FP64 rows:
 // the distributed frame's gather payload (rt_dist.hip).
 int frame_trace_paper_codes(rt_frame* f, int ri0, int ri1, uint8_t* codes_rows_dev, void* hip_stream);
+
 }  // namespace rtamd

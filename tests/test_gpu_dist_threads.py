@@ -60,10 +60,12 @@ def _others(world, k):
 @pytest.mark.parametrize("world", WORLDS)
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_concurrent_ranks_bit_exact(gpu, name, world):
+    """Frame after frame (paper frames launch their primary blocks
+    costliest first from the second frame on)."""
     sc, mode, W, H, want = _case(gpu, name)
-    out, rc, ms, msg = gpu.dist_threads(sc, W, H, mode, world, frames=3)
+    out, rc, ms, msg = gpu.dist_threads(sc, W, H, mode, world, frames=4)
     assert (rc == 0).all(), msg
-    for f in range(3):
+    for f in range(4):
         assert np.array_equal(out[f], want), f"frame {f}"
     out8, rc8, _, msg8 = gpu.dist_threads(sc, W, H, mode, world, frames=1, rgb8=True)
     assert (rc8 == 0).all(), msg8
