@@ -228,11 +228,15 @@ enum rt_flags {
     RT_FLAG_FP32 = 4,           /* NON-PARITY fast path: trace in
                                    FP32 on float copies of the scene; framebuffer stays
                                    double.  Not within the 1e-5 parity tolerance.   */
-    RT_FLAG_NO_BVH = 8          /* scenes of more than 256 top-level objects (the wave
+    RT_FLAG_NO_BVH = 8,         /* scenes of more than 256 top-level objects (the wave
                                    BVH threshold kWaveBvhMin, scene_compile.hpp) and no
                                    eager programs: wave-level culling without the wave
                                    BVH (A/B; results are identical).  No effect on
                                    smaller scenes, which never build the BVH.        */
+    RT_FLAG_FORCE_BVH = 16      /* a scene that has a wave BVH uses it on every frame.
+                                   Without this flag (or RT_FLAG_NO_BVH) the first two
+                                   frames of a frame shape try it on and off and later
+                                   frames take the faster (identical results). */
 };
 
 /* Tracer::render: render the whole frame into a caller-owned host buffer of

@@ -134,6 +134,16 @@ struct DBuf {
 struct SceneCache {
     bool valid = false;
     uint64_t uid = 0;
+    // Wave BVH on or off, decided per scene by measurement (scenes that have
+    // one: > kWaveBvhMin objects).  Exact either way (the BVH kernels equal
+    // the flat-list ones bit for bit), so the first frame of a frame shape
+    // runs with the BVH, the second without, and later frames take the one
+    // whose trace kernels were faster: a scene bound by its closest-hit ties
+    // ran 0.85x with the BVH (profiles/r04fin_bvh_perf.txt).
+    int bvh_trial = 0;       // 0: next frame tries the BVH, 1: tries without, 2: decided
+    float bvh_ms[2] = {0.f, 0.f};
+    bool bvh_off = false;
+    uint64_t bvh_key = 0;    // frame shape of the trial (W, H, mode, rows, flags)
     bool fp32 = false;
     rtamd::CompiledScene cs;
     std::vector<rt_node> nodes;   // host sources of the uploads (kept alive)
@@ -146,6 +156,13 @@ struct SceneCache {
     std::vector<rtamd::DLightR<float>> dlights_f;
     std::vector<rtamd::FoldLeafR<float>> fold_f;
 };
+
+// RT_BVH_AB (measurement A/B; default 1): 0 = a scene with a wave BVH always
+// uses it (no trial frames, SceneCache::bvh_trial).
+bool bvh_ab() {
+    static const bool on = [] { const char* e = std::getenv("RT_BVH_AB"); return !(e && *e == '0'); }();
+    return on;
+}
 
 // Per-device workspace (one render at a time per device; guarded by a mutex).
 struct Workspace {
@@ -234,6 +251,7 @@ struct rt_frame {
     bool big = false;                          // big-stack kernels (rtdb)
     bool traced = false;
     bool timed = false;                        // paper mode: a launch stored its waves' ticks (PaperParams::gtime)
+    int bvh_trial = -1;                        // SceneCache::bvh_trial this frame measures (-1: none)
     std::vector<int32_t> rows;
     std::vector<int32_t> rows_jrow;            // standard mode: rows | jitter row of each
     std::chrono::steady_clock::time_point t_start;
@@ -452,6 +470,8 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         sc.uid = rtamd::scene_uid(s);
         sc.fp32 = fp32;
         sc.valid = true;
+        sc.bvh_trial = 0;   // (a new scene: its own BVH trial)
+        sc.bvh_key = 0;
     }
     const rtamd::CompiledScene& cs = sc.cs;
     bool secondary = false;
@@ -523,6 +543,17 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.wchunk = ws.wchunk.as<float>();
     S.n_wobjs = (int)cs.wobjs.size();
     S.n_chunks = (flags & RT_FLAG_NO_BVH) ? 0 : (int)(cs.wchunk.size() / 8);
+    f->bvh_trial = -1;
+    if (S.n_chunks > 0 && !(flags & (RT_FLAG_NO_CULL | RT_FLAG_FORCE_BVH)) && bvh_ab()) {
+        const uint64_t key = ((uint64_t)(uint32_t)W << 40) ^ ((uint64_t)(uint32_t)H << 20) ^ ((uint64_t)n_rows << 2) ^
+                             ((uint64_t)mode << 1) ^ ((uint64_t)(uint32_t)flags << 48);
+        if (sc.bvh_key != key) {
+            sc.bvh_key = key;
+            sc.bvh_trial = 0;
+        }
+        if (sc.bvh_trial < 2) f->bvh_trial = sc.bvh_trial;
+        if (sc.bvh_trial == 1 || (sc.bvh_trial == 2 && sc.bvh_off)) S.n_chunks = 0;
+    }
     S.n_lights = d.n_lights;
     S.n_objs = (int)cs.objs.size();
     S.n_bounded = 0;
@@ -894,6 +925,15 @@ int frame_end_body(rt_frame* f, rt_stats* stats) {
                 for (size_t i = 0; i < 8 && e < 0; ++i) e = L[8 * g + i];
                 if (e >= 0) cost[e] = std::max(1u, (unsigned)gc[c.first / 8 + g]);
             }
+        }
+    }
+    if (f->bvh_trial >= 0) {
+        // the BVH trial frames: their trace kernels' time decides later frames
+        SceneCache& sc = ws.sc;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ws.ev[1], ws.ev[2]) == hipSuccess && sc.bvh_trial == f->bvh_trial) {
+            sc.bvh_ms[f->bvh_trial] = ms;
+            if (++sc.bvh_trial == 2) sc.bvh_off = sc.bvh_ms[1] < sc.bvh_ms[0];
         }
     }
     if (stats) {

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -519,7 +520,11 @@ public:
             if (cs.objs[j].kind != OBJ_GROUP && cs.objs[j].kind != OBJ_NEVER) ids.push_back((int)j);
         // (up to four chunks the transposed object test alone is as cheap:
         // 145 objects ran 8 % slower with the BVH, profiles/r03g_bvh_perf.txt)
-        if (cs.has_eager || (int)ids.size() <= kWaveBvhMin) return;
+        static const int bvh_min = [] {   // RT_BVH_MIN: measurement override of kWaveBvhMin
+            const char* e = std::getenv("RT_BVH_MIN");
+            return e && *e ? std::atoi(e) : kWaveBvhMin;
+        }();
+        if (cs.has_eager || (int)ids.size() <= bvh_min) return;
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int j : ids)
             if (cs.objs[j].has_bound)

@@ -40,6 +40,7 @@ RT_FLAG_COUNT_OPS = 1
 RT_FLAG_NO_CULL = 2
 RT_FLAG_FP32 = 4   # non-parity FP32 fast path
 RT_FLAG_NO_BVH = 8   # wave culls without the wave BVH (A/B; identical results)
+RT_FLAG_FORCE_BVH = 16   # the wave BVH on every frame (no on/off trial frames)
 
 NODE_SPHERE, NODE_HALFSPACE, NODE_POKEBALL, NODE_TRANSLATION, NODE_SCALING, NODE_ROTATION, NODE_CSG = range(7)
 CSG_UNION, CSG_INTERSECTION, CSG_DIFFERENCE = range(3)

@@ -136,3 +136,23 @@ def test_bvh_counts_every_object_of_every_query(gpu):
     (t_bvh, q_bvh), (t_flat, q_flat) = totals
     assert q_bvh == q_flat
     assert t_bvh == t_flat == q_bvh * n_obj
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["grid", "ties"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_bvh_on_off_trial_frames_identical(gpu, name, mode):
+    """Without RT_FLAG_FORCE_BVH / RT_FLAG_NO_BVH the first two frames of a
+    frame shape try the BVH on and off and later frames take the faster
+    (rt_render.hip SceneCache::bvh_trial): every frame across the switch is
+    bit-identical to the forced-BVH and the flat-list frames."""
+    sc = gpu.load_scene_from_json_text(json.dumps(scenes.bvh_scenes(40)[name]))
+    want, cw = _render(gpu, sc, mode, gpu.RT_FLAG_FORCE_BVH)
+    flat, cf = _render(gpu, sc, mode, gpu.RT_FLAG_NO_BVH)
+    assert cw == cf and np.array_equal(want, flat)
+    t = gpu.Tracer(sc, sc.width, sc.height, mode)
+    for i in range(4):
+        st = gpu.Stats()
+        fb = t.render(st)
+        assert np.array_equal(fb, want), i
+        assert (int(st.rays_intersect), int(st.rays_occluded)) == cw
