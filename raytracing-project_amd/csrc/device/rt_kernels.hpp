@@ -169,6 +169,43 @@ __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_
     std_body<false, false, true, C, false, WV>(S, P);   // (no directional lights: those scenes take D)
 }
 
+// apply_crosshatch (tracer.cpp:188-205) in two halves.  Its FP64 part - the
+// luminance tests - depends on the pixel's own shading only, so the primary
+// pass reduces it to a band (0: lum < 0.15, black; 1..6: the darkness branch
+// taken; 7: no branch, white; a NaN luminance takes none, as in the
+// reference) stored with the material (4 bits instead of an 8-byte
+// luminance); the finish pass applies the band's (x, y) pattern.  C++ '%'
+// truncation toward zero.
+__device__ __forceinline__ int hatch_band(real lum) {
+    if (lum < RV(0.15)) return 0;
+    const real darkness = RV(1.0) - lum;
+    if (darkness > RV(0.8)) return 1;
+    if (darkness > RV(0.65)) return 2;
+    if (darkness > RV(0.5)) return 3;
+    if (darkness > RV(0.35)) return 4;
+    if (darkness > RV(0.2)) return 5;
+    if (darkness > RV(0.12)) return 6;
+    return 7;
+}
+__device__ __forceinline__ real crosshatch(int band, int x, int y) {
+    if (band == 0) return RV(0.0);
+    const bool diag1 = ((x + y) % 4) < 1;
+    const bool diag2 = ((x - y) % 4) < 1;
+    const bool horizontal = (y % 4) < 1;
+    bool draw = false;
+    if (band == 1) draw = (diag1 && diag2) || horizontal;
+    else if (band == 2) draw = (diag1 && diag2) || (horizontal && ((x + y) % 3 == 0));
+    else if (band == 3) draw = (diag1 && diag2) || (horizontal && ((x + y) % 4 == 0));
+    else if (band == 4) draw = diag1 || (horizontal && ((x + y) % 3 == 0));
+    else if (band == 5) draw = diag1;
+    else if (band == 6) draw = diag1 && ((x + y) % 8) < 2;
+    return draw ? RV(0.0) : RV(1.0);
+}
+// material slot: material (>= -3) in the low 24 bits, band in bits 24-27
+__device__ __forceinline__ int paper_mat_pack(int mat, int band) { return (mat & 0xffffff) | (band << 24); }
+__device__ __forceinline__ int paper_mat(int slot) { return (slot << 8) >> 8; }   // (sign-extends the material)
+__device__ __forceinline__ int paper_band(int slot) { return (slot >> 24) & 15; }
+
 // Paper-mode primary records: the material slot of a pixel whose ray hit
 // nothing (a hit's material is an index >= 0, or -1 for none).
 constexpr int kPaperMiss = -3;
@@ -221,9 +258,9 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         P.nx[idx] = h.n.x;
         P.ny[idx] = h.n.y;
         P.nz[idx] = h.n.z;
-        P.mat[idx] = hits ? h.mat : kPaperMiss;   // (the finish pass's hit flag)
         sh = P.ext_shade[ei] != 0;   // (a neighbour-only row needs the hit, not the shading)
     }
+    int band = 0;   // the pixel's crosshatch band (hatch_band; neighbour-only rows: unused)
     // trace_paper (tracer.cpp:111-120) + get_luminance (:123-125).  shade()
     // runs with the whole wave (lanes with nothing to shade pass valid =
     // false) so that the wave-level shadow culls keep a full wave even when
@@ -233,9 +270,12 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         V3 base = shade<E, D, DL, WV, true>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
         if (sh) {
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
-            P.lum[idx] = RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z;
+            band = hatch_band(RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z);
         }
     }
+    // the material slot: the material (kPaperMiss for no hit: the finish
+    // pass's hit flag) in the low 24 bits, the crosshatch band above
+    if (active) P.mat[idx] = paper_mat_pack(hits ? h.mat : kPaperMiss, band);
     flush_counters(P.counters, ni, no, cnt);
     if (P.gtime && __lane_id() == 0) paper_wave_slot(P)[1] = (unsigned)wall_clock64();
 }
@@ -251,29 +291,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAV
     paper_primary_body<false, false, C, false, WV>(S, P);
 }
 
-// apply_crosshatch (tracer.cpp:188-205); C++ '%' truncation toward zero.
-__device__ __forceinline__ real crosshatch(real lum, int x, int y) {
-    if (lum < RV(0.15)) return RV(0.0);
-    const real darkness = RV(1.0) - lum;
-    const bool diag1 = ((x + y) % 4) < 1;
-    const bool diag2 = ((x - y) % 4) < 1;
-    const bool horizontal = (y % 4) < 1;
-    bool draw = false;
-    if (darkness > RV(0.8)) draw = (diag1 && diag2) || horizontal;
-    else if (darkness > RV(0.65)) draw = (diag1 && diag2) || (horizontal && ((x + y) % 3 == 0));
-    else if (darkness > RV(0.5)) draw = (diag1 && diag2) || (horizontal && ((x + y) % 4 == 0));
-    else if (darkness > RV(0.35)) draw = diag1 || (horizontal && ((x + y) % 3 == 0));
-    else if (darkness > RV(0.2)) draw = diag1;
-    else if (darkness > RV(0.12)) draw = diag1 && ((x + y) % 8) < 2;
-    return draw ? RV(0.0) : RV(1.0);
-}
-
 // One paper pixel (tracer.cpp:258-281) from its primary record and its four
 // neighbours' (-1,0) (1,0) (0,-1) (0,1), already loaded.  CODES: a
 // distributed frame's rank writes a paper_code byte (P.code) instead of FP64.
 template <bool CODES>
 __device__ __forceinline__ void paper_pixel(const PaperParams& P, int x, int y, int ri, int cm, real ct, V3 cn,
-                                            real clum, const int (&nm)[4], const real (&nt)[4], const real (&nnx)[4],
+                                            int cband, const int (&nm)[4], const real (&nt)[4], const real (&nnx)[4],
                                             const real (&nny)[4], const real (&nnz)[4]) {
     const bool ch = cm != kPaperMiss;
     // get_edge_strength (tracer.cpp:133-178)
@@ -315,7 +338,7 @@ __device__ __forceinline__ void paper_pixel(const PaperParams& P, int x, int y, 
     if constexpr (CODES) {
         // distributed frames: the pixel's place in the output alphabet
         // (rtamd::paper_code), decoded bit-exactly on the root after the gather
-        const bool h = edge <= RV(0.5) && crosshatch(clum, x, y) != RV(0.0);
+        const bool h = edge <= RV(0.5) && crosshatch(cband, x, y) != RV(0.0);
         P.code[(size_t)ri * P.W + x] = (uint8_t)(eidx | (valid < 4 ? 8 : 0) | (h ? 16 : 0));
         return;
     }
@@ -325,7 +348,7 @@ __device__ __forceinline__ void paper_pixel(const PaperParams& P, int x, int y, 
     } else if (edge > RV(0.5)) {
         o = v3(RV(0.2), RV(0.2), RV(0.2));
     } else {
-        const real h = crosshatch(clum, x, y);
+        const real h = crosshatch(cband, x, y);
         o = v3(h, h, h);
         if (edge > RV(0.3)) {
             const real darken = (edge - RV(0.3)) * RV(0.4);
@@ -361,14 +384,15 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
         real nt[4], nnx[4], nny[4], nnz[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            nm[i] = P.mat[nidx[i]];
+            nm[i] = paper_mat(P.mat[nidx[i]]);
             nt[i] = P.t[nidx[i]];
             nnx[i] = P.nx[nidx[i]];
             nny[i] = P.ny[nidx[i]];
             nnz[i] = P.nz[nidx[i]];
         }
-        paper_pixel<CODES>(P, x, y, ri, P.mat[ci], P.t[ci], v3(P.nx[ci], P.ny[ci], P.nz[ci]), P.lum[ci], nm, nt, nnx,
-                           nny, nnz);
+        const int mc = P.mat[ci];
+        paper_pixel<CODES>(P, x, y, ri, paper_mat(mc), P.t[ci], v3(P.nx[ci], P.ny[ci], P.nz[ci]), paper_band(mc), nm, nt,
+                           nnx, nny, nnz);
     } else {
         // rows: c = centre, u = up, d = down; pixels x and x + 1 (x even, W even:
         // every pair is 8/16-byte aligned)
@@ -387,26 +411,25 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
         const double2 zc = *reinterpret_cast<const double2*>(P.nz + ci);
         const double2 zu = *reinterpret_cast<const double2*>(P.nz + ui);
         const double2 zd = *reinterpret_cast<const double2*>(P.nz + di);
-        const double2 lc = *reinterpret_cast<const double2*>(P.lum + ci);
         const size_t li = ci - (x > 0 ? 1 : 0), rj = ci + 1 + (x + 2 < P.W ? 1 : 0);
-        const int ml = P.mat[li], mr = P.mat[rj];
+        const int ml = paper_mat(P.mat[li]), mr = paper_mat(P.mat[rj]);
         const real tl = P.t[li], tr = P.t[rj];
         const real xl = P.nx[li], xr = P.nx[rj], yl = P.ny[li], yr = P.ny[rj], zl = P.nz[li], zr = P.nz[rj];
         {
-            const int nm[4] = {ml, mc.y, mu.x, md.x};
+            const int nm[4] = {ml, paper_mat(mc.y), paper_mat(mu.x), paper_mat(md.x)};
             const real nt[4] = {tl, RV(tc.y), RV(tu.x), RV(td.x)};
             const real nnx[4] = {xl, RV(xc.y), RV(xu.x), RV(xd.x)}, nny[4] = {yl, RV(yc.y), RV(yu.x), RV(yd.x)},
                        nnz[4] = {zl, RV(zc.y), RV(zu.x), RV(zd.x)};
-            paper_pixel<CODES>(P, x, y, ri, mc.x, RV(tc.x), v3(RV(xc.x), RV(yc.x), RV(zc.x)), RV(lc.x), nm, nt, nnx,
-                               nny, nnz);
+            paper_pixel<CODES>(P, x, y, ri, paper_mat(mc.x), RV(tc.x), v3(RV(xc.x), RV(yc.x), RV(zc.x)), paper_band(mc.x),
+                               nm, nt, nnx, nny, nnz);
         }
         {
-            const int nm[4] = {mc.x, mr, mu.y, md.y};
+            const int nm[4] = {paper_mat(mc.x), mr, paper_mat(mu.y), paper_mat(md.y)};
             const real nt[4] = {RV(tc.x), tr, RV(tu.y), RV(td.y)};
             const real nnx[4] = {RV(xc.x), xr, RV(xu.y), RV(xd.y)}, nny[4] = {RV(yc.x), yr, RV(yu.y), RV(yd.y)},
                        nnz[4] = {RV(zc.x), zr, RV(zu.y), RV(zd.y)};
-            paper_pixel<CODES>(P, x + 1, y, ri, mc.y, RV(tc.y), v3(RV(xc.y), RV(yc.y), RV(zc.y)), RV(lc.y), nm, nt, nnx,
-                               nny, nnz);
+            paper_pixel<CODES>(P, x + 1, y, ri, paper_mat(mc.y), RV(tc.y), v3(RV(xc.y), RV(yc.y), RV(zc.y)),
+                               paper_band(mc.y), nm, nt, nnx, nny, nnz);
         }
     }
 }

@@ -109,12 +109,11 @@ struct PaperParams {
     const int32_t* ext_shade;    // 1 = row is rendered by this call (shade it)
     const int32_t* nbr;          // per rendered row: ext index of r-1, r, r+1 (-1 = outside frame)
     const int32_t* rows;         // rendered rows
-    int* mat;                    // [n_ext*W]: material of the primary hit, kPaperMiss for none
+    int* mat;                    // [n_ext*W]: primary hit's material (kPaperMiss for none) | crosshatch band << 24
     double* t;
     double* nx;
     double* ny;
     double* nz;
-    double* lum;
     double* fb;
     uint8_t* code;               // non-null: k_paper_finish writes paper_code bytes [n_rows*W] instead of fb
     unsigned int* gtime;         // non-null: primary waves store (start, end) wall-clock ticks (paper_wave_slot)

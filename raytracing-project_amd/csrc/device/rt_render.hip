@@ -673,7 +673,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         HIP_TRY(rtamd::upload_async(&ws.up, ws.paper_aux.p, ints.data(), ints.size() * sizeof(int32_t), st));
         const size_t npx = (size_t)f->n_ext * W;
         HIP_TRY(ws.paper_i.ensure(npx * sizeof(int)));
-        HIP_TRY(ws.paper_d.ensure(npx * 5 * sizeof(double)));
+        HIP_TRY(ws.paper_d.ensure(npx * 4 * sizeof(double)));
     }
     HIP_TRY(hipEventRecord(ws.ev[1], st));
     drain.armed = false;
@@ -795,7 +795,6 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
         P.nx = dd + npx;
         P.ny = dd + 2 * npx;
         P.nz = dd + 3 * npx;
-        P.lum = dd + 4 * npx;
         P.fb = fb;
         P.code = codes;
         P.gtime = nullptr;
