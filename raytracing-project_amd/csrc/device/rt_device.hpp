@@ -2694,7 +2694,7 @@ struct Frame {
 // kernel's register peak; kept live there they cost ~320 B/lane of spill slots
 // and 32 % on a frame without bounces.
 template <bool EAGER, bool DEEP, bool DL, int WV, class CT>
-__device__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+__device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     Frame stk[kMaxDepth];
     // The ray each step traces lives in memory, not registers: slot k < sp is
     // the next ray of frame k (its reflected child, later its refracted one),
@@ -2710,16 +2710,20 @@ __device__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t
     stk[0].total = v3(RV(0.0), RV(0.0), RV(0.0));   // (a finished path's colour is parked in stk[0].total)
     bool alive = true;
     const bool wave_ok = __builtin_amdgcn_read_exec() == ~0ull;
-    bool first_step = true;
-    while (__any(alive)) {
+    // One step of the wave, inlined twice: FIRST is the camera ray's step,
+    // peeled off the loop, so a wave none of whose lanes descends never enters
+    // the loop and the loop's live state does not shape that step's code (the
+    // no-bounce frame 9.81 -> 9.18 ms, the recursion row 19.16 -> 18.43 ms;
+    // profiles/r05_ab/ab_secw_peel.txt).
+    auto step = [&](auto first_tag) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_tag)::value;
         // ---- evaluate node (r, depth) on the lanes still tracing
-        const DRay r = nxt[rsel];
+        const DRay r = FIRST ? r0 : nxt[rsel];
         const bool eval = alive && depth < limit;
-        if (!first_step) {
+        if (!FIRST) {
             cnt.ev(EV_BOUNCE);
             cnt.evn(EV_COMPACT_LEAF, (unsigned)__builtin_popcountll(__ballot(eval)));
         }
-        first_step = false;
         real ht = RV(0.0);
         DHit h;
         h.p = h.n = v3(RV(0.0), RV(0.0), RV(0.0));
@@ -2823,13 +2827,15 @@ __device__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t
                 stk[0].total = ret;   // (sp == 0: the stack is free)
             }
         }
-    }
+    };
+    step(std::true_type{});
+    while (__any(alive)) step(std::false_type{});
     return stk[0].total;
 }
 
 // Tracer::trace_recursive (tracer.cpp:22-73) as an explicit frame stack.
 template <bool EAGER, bool DEEP, bool SECONDARY, bool DL, int WV, class CT>
-__device__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
+__device__ __forceinline__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
 #ifndef RT_OLD_TRACE
     if constexpr (SECONDARY && WV) return trace_wave<EAGER, DEEP, DL, WV>(S, r, n_isect, n_occl, cnt);
 #endif

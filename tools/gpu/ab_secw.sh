@@ -1,11 +1,13 @@
-# A/B of the recursion kernel: head vs cur on config 6 and the no-bounce base (tools/secw_base.py), recursion tests first.
+# A/B of the recursion kernel: head vs cur (and lib/exp/librtamd_<name>.so for each name given) on config 6
+# and the no-bounce base (tools/secw_base.py), recursion tests first.
 set -o pipefail
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_recursion.py tests/test_gpu_parity.py tests/test_gpu_deep.py -m gpu -x -q --timeout 300 --timeout-method thread 2>&1 | tail -2 || exit 1
-for v in head cur; do
+for v in head cur "$@"; do
   case $v in
     cur) L=$PWD/raytracing-project_amd/lib/librtamd.so ;;
     head) L=$PWD/raytracing-project_amd/lib/librtamd_head.so ;;
+    *) L=$PWD/raytracing-project_amd/lib/exp/librtamd_$v.so ;;
   esac
   echo "== $v"
   RTAMD_LIB=$L timeout -k 10 300 python tools/secw_base.py 2>&1 | grep -v amdgpu.ids || exit 1

@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 T=${TAG:-r02}
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${T}_gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${T}_gpu_tests.log; exit 1; }
 tail -2 gpurun_out/${T}_gpu_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/${T}_smoke.log; exit 1; }
 tail -1 gpurun_out/${T}_smoke.log
