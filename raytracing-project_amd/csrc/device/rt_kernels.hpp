@@ -285,8 +285,11 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
     paper_primary_body<E, D, C>(S, P);
 }
 
+#ifndef RT_PAPER_WAVES
+#define RT_PAPER_WAVES RT_LEAN_WAVES
+#endif
 template <bool C, int WV>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_paper_primary_lean(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PAPER_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
     paper_primary_body<false, false, C, false, WV>(S, P);
 }
