@@ -218,7 +218,10 @@ __device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
     return P.gtime + 2 * ((size_t)g * (2 * gridDim.x) + xt);
 }
 
-template <bool E, bool D, bool C, bool DL = true, int WV = 0>
+#ifndef RT_PAPER_UO
+#define RT_PAPER_UO true
+#endif
+template <bool E, bool D, bool C, bool DL = true, int WV = 0, bool T = false>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
@@ -228,11 +231,18 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     // (list entries < 0 pad a run of consecutive rows to a wave boundary)
     const int ei = li < P.n_list ? P.ext_list[li] : -1;
     const bool active = x < P.W && ei >= 0;
-    // the wave's cost for the next frame's launch order (rt_render.hip
-    // order_paper_groups): its start and end wall-clock ticks, stored into
-    // its own slot (nothing held across the kernel; one-address atomics per
-    // list group serialised the waves: +18 % frame time)
-    if (P.gtime && __lane_id() == 0) paper_wave_slot(P)[0] = (unsigned)wall_clock64();
+    // T (timed launches, P.gtime set): the wave's cost for later frames'
+    // launch order (rt_render.hip order_paper_groups), its start and end
+    // wall-clock ticks, stored into its own slot at the end (one-address
+    // atomics per list group serialised the waves: +18 % frame time).  Every
+    // store of this kernel comes after its last scene read, and only timed
+    // launches read the clock at the start: a global store or the clock read
+    // (an intrinsic with side effects) ahead of a load from the scene's arrays
+    // takes away the compiler's proof that the load sees unmodified memory,
+    // and the wave-uniform object and node reads of every shadow query then
+    // become vector loads instead of scalar ones (config 5 4.61 vs 5.30 ms).
+    unsigned t_start = 0u;
+    if constexpr (T) t_start = (unsigned)wall_clock64();
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
     cnt.init();
@@ -254,10 +264,6 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         else
             hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
         idx = (size_t)ei * P.W + x;
-        P.t[idx] = ht;
-        P.nx[idx] = h.n.x;
-        P.ny[idx] = h.n.y;
-        P.nz[idx] = h.n.z;
         sh = P.ext_shade[ei] != 0;   // (a neighbour-only row needs the hit, not the shading)
     }
     int band = 0;   // the pixel's crosshatch band (hatch_band; neighbour-only rows: unused)
@@ -267,7 +273,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     // it mixes shaded rows and neighbour-only rows (strip edges of a
     // multi-GPU partition) or inactive lanes.
     if (__any(sh)) {
-        V3 base = shade<E, D, DL, WV, true>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
+        V3 base = shade<E, D, DL, WV, RT_PAPER_UO>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
         if (sh) {
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             band = hatch_band(RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z);
@@ -275,23 +281,35 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     }
     // the material slot: the material (kPaperMiss for no hit: the finish
     // pass's hit flag) in the low 24 bits, the crosshatch band above
-    if (active) P.mat[idx] = paper_mat_pack(hits ? h.mat : kPaperMiss, band);
+    if (active) {
+        P.t[idx] = ht;
+        P.nx[idx] = h.n.x;
+        P.ny[idx] = h.n.y;
+        P.nz[idx] = h.n.z;
+        P.mat[idx] = paper_mat_pack(hits ? h.mat : kPaperMiss, band);
+    }
     flush_counters(P.counters, ni, no, cnt);
-    if (P.gtime && __lane_id() == 0) paper_wave_slot(P)[1] = (unsigned)wall_clock64();
+    if constexpr (T) {
+        if (__lane_id() == 0) {
+            unsigned* slot = paper_wave_slot(P);
+            slot[0] = t_start;
+            slot[1] = (unsigned)wall_clock64();
+        }
+    }
 }
 
-template <bool E, bool D, bool C>
+template <bool E, bool D, bool C, bool T = false>
 __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
-    paper_primary_body<E, D, C>(S, P);
+    paper_primary_body<E, D, C, true, 0, T>(S, P);
 }
 
 #ifndef RT_PAPER_WAVES
 #define RT_PAPER_WAVES RT_LEAN_WAVES
 #endif
-template <bool C, int WV>
+template <bool C, int WV, bool T = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PAPER_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
-    paper_primary_body<false, false, C, false, WV>(S, P);
+    paper_primary_body<false, false, C, false, WV, T>(S, P);
 }
 
 // One paper pixel (tracer.cpp:258-281) from its primary record and its four
@@ -483,7 +501,9 @@ void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const St
 
 template <bool E, bool D>
 void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
+    // (timed launches: never op-counting ones, rt_frame_trace)
     if (c) hipLaunchKernelGGL((k_paper_primary<E, D, true>), grid, dim3(256), 0, st, S, P);
+    else if (P.gtime) hipLaunchKernelGGL((k_paper_primary<E, D, false, true>), grid, dim3(256), 0, st, S, P);
     else hipLaunchKernelGGL((k_paper_primary<E, D, false>), grid, dim3(256), 0, st, S, P);
 }
 
@@ -546,12 +566,15 @@ void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const Scene
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
     else if (bv) {
         if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 2>), grid, dim3(256), 0, st, S, P);
+        else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, 2, true>), grid, dim3(256), 0, st, S, P);
         else hipLaunchKernelGGL((k_paper_primary_lean<false, 2>), grid, dim3(256), 0, st, S, P);
     } else if (wv) {
         if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 1>), grid, dim3(256), 0, st, S, P);
+        else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, 1, true>), grid, dim3(256), 0, st, S, P);
         else hipLaunchKernelGGL((k_paper_primary_lean<false, 1>), grid, dim3(256), 0, st, S, P);
     } else {
         if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 0>), grid, dim3(256), 0, st, S, P);
+        else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, 0, true>), grid, dim3(256), 0, st, S, P);
         else hipLaunchKernelGGL((k_paper_primary_lean<false, 0>), grid, dim3(256), 0, st, S, P);
     }
 #endif

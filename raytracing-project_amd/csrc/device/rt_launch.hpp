@@ -116,7 +116,7 @@ struct PaperParams {
     double* nz;
     double* fb;
     uint8_t* code;               // non-null: k_paper_finish writes paper_code bytes [n_rows*W] instead of fb
-    unsigned int* gtime;         // non-null: primary waves store (start, end) wall-clock ticks (paper_wave_slot)
+    unsigned int* gtime;         // non-null: a timed launch; primary waves store (start, end) wall-clock ticks (paper_wave_slot)
     unsigned long long* counters;
 };
 

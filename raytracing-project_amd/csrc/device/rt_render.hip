@@ -806,14 +806,16 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
                 return RT_ERR_PROCESSING;
             }
             // RT_PAPER_ORDER (measurement A/B): 0 = row order, untimed; 1 = row
-            // order, timed; 2 (default) = costliest blocks first
+            // order, every frame timed; 2 (default) = costliest blocks first,
+            // from the wave times of the first frame of the scene and row set
+            // (later frames untimed: a timed launch reads the clock ahead of
+            // the scene loads, which costs it its scalar loads, k_paper_primary_lean)
             static const int order_mode = [] { const char* e = std::getenv("RT_PAPER_ORDER"); return e && *e ? std::atoi(e) : 2; }();
-            if (order_mode >= 2) {
-                const auto it = ws.paper_cost.find(f->key);
-                order_paper_groups(list, it == ws.paper_cost.end() ? nullptr : &it->second);
-            }
+            const auto cost_it = ws.paper_cost.find(f->key);
+            const bool have_cost = cost_it != ws.paper_cost.end();
+            if (order_mode >= 2) order_paper_groups(list, have_cost ? &cost_it->second : nullptr);
             P.n_list = (int)list.size();
-            if (order_mode >= 1) {
+            if (!f->count_ops && (order_mode == 1 || (order_mode >= 2 && !have_cost))) {
                 P.gtime = ws.gtime.as<unsigned>() + (size_t)(f->list_used / 8) * paper_waves_per_group(W) * 2;
                 f->timed = true;
             }
