@@ -117,7 +117,11 @@ std::vector<int> strip_owners(int n_strips, int world, int mode, int kind) {
     std::vector<int> own((size_t)std::max(0, n_strips), 0);
     if (world <= 1) return own;
     std::vector<int64_t> w((size_t)world, 1000), cur((size_t)world, 0);
-    const int64_t c = kind ? 0 : (mode == RT_MODE_PAPER ? kRootShedPaper : kRootShedStd);
+    // (RT_ROOT_SHED_PAPER / RT_ROOT_SHED_STD: measurement A/B only; every rank
+    // of a job must see the same value - the frame descriptor does not carry it)
+    static const int shed_paper = [] { const char* e = std::getenv("RT_ROOT_SHED_PAPER"); return e && *e ? std::atoi(e) : kRootShedPaper; }();
+    static const int shed_std = [] { const char* e = std::getenv("RT_ROOT_SHED_STD"); return e && *e ? std::atoi(e) : kRootShedStd; }();
+    const int64_t c = kind ? 0 : (mode == RT_MODE_PAPER ? shed_paper : shed_std);
     w[0] = std::max<int64_t>(500, 1000 - c * world);
     int64_t total = 0;
     for (int64_t v : w) total += v;
@@ -729,7 +733,6 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     // too.
     int64_t* xd = D.xchg.as<int64_t>();
     int64_t* xh = D.xchg_host;
-    bool agreed = !coll;
     auto issue_agreement = [&]() -> bool {
         const int64_t v[kDescFields] = {W, H, mode, kind, flags, shash};
         for (int i = 0; i < kDescFields; ++i) {
@@ -769,9 +772,18 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     };
     double* fb_rows = direct ? static_cast<double*>(out_root) : D.mine.as<double>();
     int n_tb = 0, n_g = 0;
-    bool status_sent = false;
+    bool status_sent = false, issued = false;
+    // Pass 1: every chunk's trace (and toByte) enqueued on its stream and the
+    // chunk's end recorded (ev_chunk[k]); agreement 1 issued right after
+    // chunk 0.  Pass 2 (collective frames): agreement 1's verdict, agreement 2
+    // (this rank's trace status: every enqueue is known by then, so the
+    // reduction sits on the collective stream ahead of the gathers, in the
+    // shadow of the trace, not between the last two gathers at the frame's
+    // tail), then one gather (+ the root's placement) per chunk.
+    bool chunk_ev[kChunks] = {};
     for (size_t k = 0; k < bounds.size(); ++k) {
         const int a = bounds[k].first, b = bounds[k].second, hi = std::min(b, n);
+        (void)b;
         // chunks alternate between two streams, the last one on st: the frame's
         // end (rt_frame_end on st) then follows it in stream order instead of
         // through a cross-queue wait (~40 us, profiles/r04u_api_timeline.txt)
@@ -794,40 +806,51 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             if (rc != RT_OK) break;
             continue;
         }
-        if (!agreed) {
-            if (!issue_agreement()) return RT_ERR_HIP;
-            // (the descriptor reduction runs while chunk 0 traces)
-            const int rw = dist_wait(D, D.ev_desc, "the frame agreement");
-            if (rw != RT_OK) {
-                if (f) (void)rt_frame_end(f, nullptr);
-                return rw;
-            }
-            std::string bad;
-            for (int i = 0; i < kDescFields; ++i) {
-                static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags", "scene"};
-                if (xh[i] != -xh[kDescFields + i]) bad += std::string(bad.empty() ? "" : ", ") + names[i];
-            }
-            std::string failed;
-            for (int r = 0; r < D.world; ++r)
-                if (xh[2 * kDescFields + r]) failed += (failed.empty() ? "" : ",") + std::to_string(r);
-            if (!bad.empty() || !failed.empty()) {
-                // every rank reaches this same verdict: no gather is issued anywhere
-                const int rl = rc;
-                const int re = f ? rt_frame_end(f, nullptr) : RT_OK;
-                (void)re;
-                if (rl != RT_OK) return rl;   // this rank's own failure (message already set)
-                if (!bad.empty()) {
-                    rtamd::set_last_error("rt_render_dist: the ranks disagree on the frame (" + bad + ")");
-                    return RT_ERR_INVALID_ARG;
-                }
-                rtamd::set_last_error("rt_render_dist: rank(s) " + failed + " failed to set up or start the frame");
-                return RT_ERR_HIP;
-            }
-            agreed = true;
+        // chunk k's end, for its gather (none after a local failure: the
+        // gather is still issued - the peers are waiting for it)
+        if (rc == RT_OK) {
+            chunk_ev[k] = hipEventRecord(D.ev_chunk[k], cst) == hipSuccess;
+            if (!chunk_ev[k]) fail(RT_ERR_HIP, "event chaining failed");
         }
-        // agreement 2: this rank's trace status, issued before the last
-        // gather (known here: the last chunk's trace is enqueued or skipped)
-        if (k + 1 == bounds.size()) {
+        if (!issued) {
+            if (!issue_agreement()) return RT_ERR_HIP;
+            issued = true;
+        }
+    }
+    if (coll && !issued) {
+        if (!issue_agreement()) return RT_ERR_HIP;
+        issued = true;
+    }
+    if (coll) {
+        // (the descriptor reduction ran while the chunks trace)
+        const int rw = dist_wait(D, D.ev_desc, "the frame agreement");
+        if (rw != RT_OK) {
+            if (f) (void)rt_frame_end(f, nullptr);
+            return rw;
+        }
+        std::string bad;
+        for (int i = 0; i < kDescFields; ++i) {
+            static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags", "scene"};
+            if (xh[i] != -xh[kDescFields + i]) bad += std::string(bad.empty() ? "" : ", ") + names[i];
+        }
+        std::string failed;
+        for (int r = 0; r < D.world; ++r)
+            if (xh[2 * kDescFields + r]) failed += (failed.empty() ? "" : ",") + std::to_string(r);
+        if (!bad.empty() || !failed.empty()) {
+            // every rank reaches this same verdict: no gather is issued anywhere
+            const int rl = rc;
+            const int re = f ? rt_frame_end(f, nullptr) : RT_OK;
+            (void)re;
+            if (rl != RT_OK) return rl;   // this rank's own failure (message already set)
+            if (!bad.empty()) {
+                rtamd::set_last_error("rt_render_dist: the ranks disagree on the frame (" + bad + ")");
+                return RT_ERR_INVALID_ARG;
+            }
+            rtamd::set_last_error("rt_render_dist: rank(s) " + failed + " failed to set up or start the frame");
+            return RT_ERR_HIP;
+        }
+        // agreement 2: this rank's trace status (every chunk is enqueued or skipped)
+        {
             int64_t* sd = xd + n_desc;
             int64_t* sh = xh + n_desc;
             for (int r = 0; r < D.world; ++r) sh[r] = (r == D.rank && rc != RT_OK) ? 1 : 0;
@@ -838,31 +861,33 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             if (!ok) fail(RT_ERR_HIP, ("trace status reduction could not be issued: " + why).c_str());
             status_sent = ok;
         }
-        // chunk k -> root: ONE collective, ordered after the chunk's trace
-        // (issued whatever happened locally: the peers are waiting for it)
-        if (rc == RT_OK && (hipEventRecord(D.ev_chunk[k], cst) != hipSuccess ||
-                            hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess))
-            fail(RT_ERR_HIP, "event chaining failed");
-        const bool timed = hipEventRecord(D.ev_gs[n_g], D.comm_st) == hipSuccess;
-        const char* send = (kind && !codes ? D.mine8.as<char>() : D.mine.as<char>()) + (size_t)a * row_bytes;
-        const size_t chunk_bytes = (size_t)(b - a) * row_bytes;
-        char* recv = stage.as<char>() + (size_t)D.world * a * row_bytes;
-        {
-            const std::string why = coll_gather(D, send, (root || D.sim_stage) ? recv : nullptr, chunk_bytes,
-                                                kind || codes, "a gather");
-            if (!why.empty()) {
-                fail(RT_ERR_HIP, why.c_str());
-                if (D.simg && D.simg->is_aborted(nullptr)) dist_abort(D, why);
+        for (size_t k = 0; k < bounds.size(); ++k) {
+            const int a = bounds[k].first, b = bounds[k].second;
+            // chunk k -> root: ONE collective, ordered after the chunk's trace
+            // (issued whatever happened locally: the peers are waiting for it)
+            if (chunk_ev[k] && hipStreamWaitEvent(D.comm_st, D.ev_chunk[k], 0) != hipSuccess)
+                fail(RT_ERR_HIP, "event chaining failed");
+            const bool timed = hipEventRecord(D.ev_gs[n_g], D.comm_st) == hipSuccess;
+            const char* send = (kind && !codes ? D.mine8.as<char>() : D.mine.as<char>()) + (size_t)a * row_bytes;
+            const size_t chunk_bytes = (size_t)(b - a) * row_bytes;
+            char* recv = stage.as<char>() + (size_t)D.world * a * row_bytes;
+            {
+                const std::string why = coll_gather(D, send, (root || D.sim_stage) ? recv : nullptr, chunk_bytes,
+                                                    kind || codes, "a gather");
+                if (!why.empty()) {
+                    fail(RT_ERR_HIP, why.c_str());
+                    if (D.simg && D.simg->is_aborted(nullptr)) dist_abort(D, why);
+                }
             }
+            if (root) {
+                const int32_t* slots = D.rowtab.as<int32_t>() + (size_t)D.world * a;
+                const hipError_t pe = codes ? place_codes(reinterpret_cast<const uint8_t*>(recv), slots, D.world * (b - a),
+                                                          Wc, kind, out_root, D.comm_st)
+                                            : place_rows(recv, slots, D.world * (b - a), row_bytes, out_root, D.comm_st);
+                if (pe != hipSuccess) fail(RT_ERR_HIP, "row placement failed");
+            }
+            if (timed && hipEventRecord(D.ev_ge[n_g], D.comm_st) == hipSuccess) ++n_g;
         }
-        if (root) {
-            const int32_t* slots = D.rowtab.as<int32_t>() + (size_t)D.world * a;
-            const hipError_t pe = codes ? place_codes(reinterpret_cast<const uint8_t*>(recv), slots, D.world * (b - a),
-                                                      Wc, kind, out_root, D.comm_st)
-                                        : place_rows(recv, slots, D.world * (b - a), row_bytes, out_root, D.comm_st);
-            if (pe != hipSuccess) fail(RT_ERR_HIP, "row placement failed");
-        }
-        if (timed && hipEventRecord(D.ev_ge[n_g], D.comm_st) == hipSuccess) ++n_g;
     }
     // alt_st's last work (a chunk's toByte) into st, which rt_frame_end
     // synchronises (without toByte, rt_frame_end joins alt_st's last trace call)

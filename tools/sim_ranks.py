@@ -206,6 +206,7 @@ def product_ranks(args):
                "max_rank_wall_ms": round(worst, 3), "rank0_wall_ms": round(per[0]["wall_ms"], 3),
                "min_rank_wall_ms": round(min(p["wall_ms"] for p in per), 3),
                "max_rank_kernel_ms": round(max(p["kernel_ms"] for p in per), 3),
+               "rank_wall_ms": [round(p["wall_ms"], 3) for p in per],
                "gather_bytes_per_rank": m * W * bpp,
                "speedup_before_gather": round(base / worst, 3) if base else None,
                "last_chunk_place_ms": round(place_ms, 4),
