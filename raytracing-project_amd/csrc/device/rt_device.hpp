@@ -2693,17 +2693,27 @@ struct Frame {
 // point and the normal are dead across shade(), whose shadow queries set the
 // kernel's register peak; kept live there they cost ~320 B/lane of spill slots
 // and 32 % on a frame without bounces.
+// trace_wave's frame: the colour so far and the material; the children's
+// rays live in the ray slots (two per level), so a frame is 32 bytes.  The
+// stack sits in scratch, and every resident wave's stack lines travel
+// through the L2 (profiles/r05u_pmc_mem_cfg6.txt): frames are kept small and
+// nothing is copied between slots.
+struct WFrame {
+    V3 total;
+    int mat;
+    int sf;   // bit 0: stage (0 = reflection child pending, 1 = refraction child pending); bit 1: refraction wanted
+};
+
 template <bool EAGER, bool DEEP, bool DL, int WV, class CT>
 __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
-    Frame stk[kMaxDepth];
-    // The ray each step traces lives in memory, not registers: slot k < sp is
-    // the next ray of frame k (its reflected child, later its refracted one),
-    // slot kMaxDepth the camera ray.  A step loads it, and it is dead by the
-    // time the step is shaded (a loop-carried register copy stayed live
-    // across shade() on every path).
-    DRay nxt[kMaxDepth + 1];
-    nxt[kMaxDepth] = r0;
-    int rsel = kMaxDepth;
+    WFrame stk[kMaxDepth];
+    // The ray each step traces lives in memory, not registers: slots 2k and
+    // 2k + 1 hold frame k's reflected and refracted children.  A step after
+    // the camera ray's loads its ray from slot rsel (lanes with nothing to
+    // evaluate load nothing), and it is dead by the time the step is shaded
+    // (a loop-carried register copy stayed live across shade() on every path).
+    DRay nxt[2 * kMaxDepth];
+    int rsel = 0;
     int sp = 0;
     int depth = 0;
     const int limit = S.rec_limit;
@@ -2718,8 +2728,14 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
     auto step = [&](auto first_tag) __attribute__((always_inline)) {
         constexpr bool FIRST = decltype(first_tag)::value;
         // ---- evaluate node (r, depth) on the lanes still tracing
-        const DRay r = FIRST ? r0 : nxt[rsel];
         const bool eval = alive && depth < limit;
+        DRay r;
+        if constexpr (FIRST) {
+            r = r0;
+        } else {
+            r = DRay{v3(RV(0.0), RV(0.0), RV(0.0)), v3(RV(0.0), RV(0.0), -RV(1.0))};   // (riders: never traced)
+            if (eval) r = nxt[rsel];
+        }
         if (!FIRST) {
             cnt.ev(EV_BOUNCE);
             cnt.evn(EV_COMPACT_LEAF, (unsigned)__builtin_popcountll(__ballot(eval)));
@@ -2760,10 +2776,9 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
                 }
             }
             if (want_refl || want_refr) {
-                Frame& fr = stk[sp];
+                WFrame& fr = stk[sp];
                 fr.mat = h.mat;
-                fr.want_refr = want_refr;
-                fr.refr = refr;
+                if (want_refr) nxt[2 * sp + 1] = refr;
                 cnt.inc(RT_OPC_SECONDARY);
                 if (want_refl) {
                     const V3 inc = normalized(r.d);
@@ -2771,11 +2786,10 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
                     const V3 rd = normalized(v3(inc.x - h.n.x * k, inc.y - h.n.y * k, inc.z - h.n.z * k));
                     const V3 ro = h.ff ? v3(h.p.x + h.n.x * RV(1e-6), h.p.y + h.n.y * RV(1e-6), h.p.z + h.n.z * RV(1e-6))
                                        : v3(h.p.x - h.n.x * RV(1e-6), h.p.y - h.n.y * RV(1e-6), h.p.z - h.n.z * RV(1e-6));
-                    fr.stage = 0;
-                    nxt[sp] = make_ray(ro, rd);
+                    fr.sf = want_refr ? 2 : 0;
+                    nxt[2 * sp] = make_ray(ro, rd);
                 } else {
-                    fr.stage = 1;
-                    nxt[sp] = refr;
+                    fr.sf = 1;
                 }
                 ++sp;
                 descend = true;
@@ -2791,7 +2805,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         if (sh) {
             if (descend) {
                 stk[sp - 1].total = direct;
-                rsel = sp - 1;
+                rsel = 2 * (sp - 1) + (stk[sp - 1].sf & 1);
                 depth = sp;
             } else {
                 ret = direct;
@@ -2801,15 +2815,15 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
             // ---- unwind
             bool resumed = false;
             while (sp > 0) {
-                Frame& fr = stk[sp - 1];
+                WFrame& fr = stk[sp - 1];
                 const MatT* mat = &S.mats[fr.mat];
-                if (fr.stage == 0) {
+                const int sf = fr.sf;
+                if ((sf & 1) == 0) {
                     fr.total = combine(fr.total, v3(ret.x * mat->kr, ret.y * mat->kr, ret.z * mat->kr));
-                    if (fr.want_refr) {
+                    if (sf & 2) {
                         cnt.inc(RT_OPC_SECONDARY);
-                        fr.stage = 1;
-                        nxt[sp - 1] = fr.refr;
-                        rsel = sp - 1;
+                        fr.sf = sf | 1;
+                        rsel = 2 * (sp - 1) + 1;
                         depth = sp;
                         resumed = true;
                         break;
