@@ -2717,7 +2717,8 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
     int sp = 0;
     int depth = 0;
     const int limit = S.rec_limit;
-    stk[0].total = v3(RV(0.0), RV(0.0), RV(0.0));   // (a finished path's colour is parked in stk[0].total)
+    // (a finished path's colour is parked in stk[0].total: every lane's path
+    // finishes, so the slot is always written before the final read)
     bool alive = true;
     const bool wave_ok = __builtin_amdgcn_read_exec() == ~0ull;
     // One step of the wave, inlined twice: FIRST is the camera ray's step,
@@ -2841,8 +2842,12 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
                 stk[0].total = ret;   // (sp == 0: the stack is free)
             }
         }
+        return ret;
     };
-    step(std::true_type{});
+    // (a wave none of whose lanes descends: every lane's colour is the first
+    // step's value, returned from registers)
+    const V3 first = step(std::true_type{});
+    if (!__any(alive)) return first;
     while (__any(alive)) step(std::false_type{});
     return stk[0].total;
 }
