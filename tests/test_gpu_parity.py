@@ -202,3 +202,22 @@ def test_counting_pass_with_cull_matches_plain_midres(gpu):
     b = gpu.Tracer(sc, W, H, 0, flags=gpu.RT_FLAG_COUNT_OPS).render(s1)
     assert np.array_equal(a, b)
     assert (s0.rays_intersect, s0.rays_occluded) == (s1.rays_intersect, s1.rays_occluded)
+
+
+# Paper frames of one scene and row set: the first launches the timed primary
+# (k_paper_primary_lean<C, WV, true>: wave ticks for the launch order), later
+# ones the untimed kernel in costliest-first block order.  Every frame must be
+# the oracle's, bit for bit, with the same ray counts.
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cfg5", "pokeballs", "csg_groups"])
+def test_paper_timed_then_ordered_frames_identical(gpu, name):
+    rt = gpu
+    sc = rt.load_scene_from_json_text(SMALL[name]())
+    W, H = sc.width, sc.height
+    ref, ost = rt.oracle_render(sc, W, H, 1, threads=8)
+    tr = rt.Tracer(sc, W, H, 1)
+    for k in range(3):
+        st = rt.Stats()
+        fb = tr.render(st)
+        assert np.array_equal(fb, ref), f"frame {k}"
+        assert (st.rays_intersect, st.rays_occluded) == (ost.rays_intersect, ost.rays_occluded), f"frame {k}"
