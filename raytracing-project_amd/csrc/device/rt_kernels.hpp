@@ -390,11 +390,7 @@ __device__ __forceinline__ void paper_pixel(const PaperParams& P, int x, int y, 
 // against kPaperMiss).  PAIR (even W): a thread takes two adjacent pixels
 // with 8/16-byte loads of both, and their outer x-neighbours.
 template <bool CODES, bool PAIR>
-__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
-    const int xt = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int ri = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const int x = PAIR ? 2 * xt : xt;
-    if (x >= P.W || ri >= P.n_rows) return;
+__device__ __forceinline__ void paper_finish_px(const PaperParams& P, int x, int ri) {
     const int y = P.rows[ri];
     const int e_up = P.nbr[3 * ri + 0], e_c = P.nbr[3 * ri + 1], e_dn = P.nbr[3 * ri + 2];
     const size_t ci = (size_t)e_c * P.W + x;
@@ -452,6 +448,26 @@ __global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
             paper_pixel<CODES>(P, x + 1, y, ri, paper_mat(mc.y), RV(tc.y), v3(RV(xc.y), RV(yc.y), RV(zc.y)),
                                paper_band(mc.y), nm, nt, nnx, nny, nnz);
         }
+    }
+}
+
+// RT_FINISH_RPT row rounds per block: a 64x4-thread block finishes 4 rows per
+// round, so a round's up / down neighbour records were the previous round's
+// centre rows (L1 / L2-hot) and only a block's first and last rows are read
+// again by another block.
+#ifndef RT_FINISH_RPT
+#define RT_FINISH_RPT 1
+#endif
+constexpr int kFinishRounds = RT_FINISH_RPT;
+template <bool CODES, bool PAIR>
+__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
+    const int xt = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int x = PAIR ? 2 * xt : xt;
+    if (x >= P.W) return;
+    for (int k = 0; k < kFinishRounds; ++k) {
+        const int ri = (blockIdx.y * kFinishRounds + k) * 4 + (threadIdx.x >> 6);
+        if (ri >= P.n_rows) return;
+        paper_finish_px<CODES, PAIR>(P, x, ri);
     }
 }
 
@@ -605,7 +621,9 @@ const void* paper_kernel(bool e, bool d, bool wv, bool bv) {
 }
 
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {
-    // (grid.x covers W pixels one per thread; even W: two per thread)
+    // (grid.x covers W pixels one per thread; even W: two per thread; grid.y
+    // 4 * kFinishRounds rows per block)
+    grid.y = (P.n_rows + 4 * kFinishRounds - 1) / (4 * kFinishRounds);
     if (P.W % 2 == 0) {
         const dim3 g2((P.W / 2 + 63) / 64, grid.y);
         if (P.code) hipLaunchKernelGGL((k_paper_finish<true, true>), g2, dim3(256), 0, st, P);
