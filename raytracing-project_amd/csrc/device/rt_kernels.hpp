@@ -458,14 +458,20 @@ __device__ __forceinline__ void paper_finish_px(const PaperParams& P, int x, int
 #ifndef RT_FINISH_RPT
 #define RT_FINISH_RPT 1
 #endif
+// RT_FINISH_BR rows per block (64 x BR threads): a block's rows share their
+// neighbour rows, only its first and last rows' are read by another block
+#ifndef RT_FINISH_BR
+#define RT_FINISH_BR 4
+#endif
 constexpr int kFinishRounds = RT_FINISH_RPT;
+constexpr int kFinishRows = RT_FINISH_BR;
 template <bool CODES, bool PAIR>
-__global__ __launch_bounds__(256) void k_paper_finish(PaperParams P) {
+__global__ __launch_bounds__(64 * kFinishRows) void k_paper_finish(PaperParams P) {
     const int xt = blockIdx.x * 64 + (threadIdx.x & 63);
     const int x = PAIR ? 2 * xt : xt;
     if (x >= P.W) return;
     for (int k = 0; k < kFinishRounds; ++k) {
-        const int ri = (blockIdx.y * kFinishRounds + k) * 4 + (threadIdx.x >> 6);
+        const int ri = (blockIdx.y * kFinishRounds + k) * kFinishRows + (threadIdx.x >> 6);
         if (ri >= P.n_rows) return;
         paper_finish_px<CODES, PAIR>(P, x, ri);
     }
@@ -622,15 +628,16 @@ const void* paper_kernel(bool e, bool d, bool wv, bool bv) {
 
 void launch_paper_finish(dim3 grid, hipStream_t st, const PaperParams& P) {
     // (grid.x covers W pixels one per thread; even W: two per thread; grid.y
-    // 4 * kFinishRounds rows per block)
-    grid.y = (P.n_rows + 4 * kFinishRounds - 1) / (4 * kFinishRounds);
+    // kFinishRows * kFinishRounds rows per block)
+    grid.y = (P.n_rows + kFinishRows * kFinishRounds - 1) / (kFinishRows * kFinishRounds);
+    const dim3 blk(64 * kFinishRows);
     if (P.W % 2 == 0) {
         const dim3 g2((P.W / 2 + 63) / 64, grid.y);
-        if (P.code) hipLaunchKernelGGL((k_paper_finish<true, true>), g2, dim3(256), 0, st, P);
-        else hipLaunchKernelGGL((k_paper_finish<false, true>), g2, dim3(256), 0, st, P);
+        if (P.code) hipLaunchKernelGGL((k_paper_finish<true, true>), g2, blk, 0, st, P);
+        else hipLaunchKernelGGL((k_paper_finish<false, true>), g2, blk, 0, st, P);
     } else {
-        if (P.code) hipLaunchKernelGGL((k_paper_finish<true, false>), grid, dim3(256), 0, st, P);
-        else hipLaunchKernelGGL((k_paper_finish<false, false>), grid, dim3(256), 0, st, P);
+        if (P.code) hipLaunchKernelGGL((k_paper_finish<true, false>), grid, blk, 0, st, P);
+        else hipLaunchKernelGGL((k_paper_finish<false, false>), grid, blk, 0, st, P);
     }
 }
 
