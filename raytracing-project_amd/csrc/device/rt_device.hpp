@@ -310,7 +310,13 @@ struct DevScene {
     int cam_nx, cam_ny;
     int rec_limit, cull;
     real eye[3], P[3], Lx, Ly;
-    real bg[3], amb[3], medium_index;
+    real medium_index;
+    // The background colour (the miss value) is the albedo of material slot
+    // bg_mat, and every material's ambient term arrives multiplied by the
+    // scene's ambient (E_a = K_a I_a, shading.cpp:39: the same single
+    // multiplication, done on the host): neither is a kernel argument held in
+    // SGPRs through the whole trace.
+    int bg_mat;
     // wave BVH kernels only (objs / ctab then hold CompiledScene::wobjs /
     // wctab): each object's index in the reference's order, and the chunk
     // records (2 x float4 per chunk of 64 objects)
@@ -320,6 +326,7 @@ struct DevScene {
 };
 
 __device__ __forceinline__ V3 ld3(const real* p) { return v3(p[0], p[1], p[2]); }
+__device__ __forceinline__ V3 background(const DevScene& S) { return ld3(S.mats[S.bg_mat].albedo); }
 
 // --------------------------------------------------------------- primitives
 // Sphere::intersect (geometry.cpp:12-37)
@@ -2532,7 +2539,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
     V3 E = v3(RV(0.0), RV(0.0), RV(0.0));
     {
         const MatT* m = &S.mats[valid ? hit.mat : 0];
-        E = v3(m->ambient[0] * S.amb[0], m->ambient[1] * S.amb[1], m->ambient[2] * S.amb[2]);
+        E = v3(m->ambient[0], m->ambient[1], m->ambient[2]);   // (K_a I_a, premultiplied)
     }
     // directional lights first (shading.cpp:45-76): no falloff, shadow ray to infinity
     for (int li = 0; DL && li < S.n_dlights; ++li) {
@@ -2802,7 +2809,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         // the step's value (a finished lane's colour is in memory, so nothing
         // but the stack state is carried across steps)
         V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));
-        if (eval && !hit) ret = v3(S.bg[0], S.bg[1], S.bg[2]);
+        if (eval && !hit) ret = background(S);
         if (sh) {
             if (descend) {
                 stk[sp - 1].total = direct;
@@ -2873,14 +2880,14 @@ __device__ __forceinline__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect
             const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2)>(S, r, RV(1e-4), RT_INF, ht, h,
                                                                __builtin_amdgcn_read_exec() == ~0ull, cnt);
             cnt.pe(PH_PRIMARY);
-            if (!__any(hit)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+            if (!__any(hit)) return background(S);
 #if defined(RT_ABL) && RT_ABL == 5   // diagnostic: primary hit only, no shading
-            if (S.n_objs != 12345) return hit ? h.n : v3(S.bg[0], S.bg[1], S.bg[2]);
+            if (S.n_objs != 12345) return hit ? h.n : background(S);
 #endif
             const V3 E = shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt, hit);
-            return hit ? E : v3(S.bg[0], S.bg[1], S.bg[2]);
+            return hit ? E : background(S);
         } else {
-            if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) return v3(S.bg[0], S.bg[1], S.bg[2]);
+            if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) return background(S);
             return shade<EAGER, DEEP, DL, WV>(S, ht, h, normalized(vneg(r.d)), n_occl, cnt);
         }
     }
@@ -2899,7 +2906,7 @@ __device__ __forceinline__ V3 trace(const DevScene& S, DRay r, uint32_t& n_isect
             DHit h;
             ++n_isect;
             if (!scene_intersect<EAGER, DEEP>(S, r, RV(1e-4), RT_INF, ht, h, cnt)) {
-                ret = v3(S.bg[0], S.bg[1], S.bg[2]);
+                ret = background(S);
             } else {
                 const V3 wo = normalized(vneg(r.d));
                 const V3 direct = shade<EAGER, DEEP, DL, WV>(S, ht, h, wo, n_occl, cnt);

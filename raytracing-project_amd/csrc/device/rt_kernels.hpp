@@ -506,12 +506,11 @@ DevScene make_scene(const SceneView& V, bool bv = false) {
     for (int i = 0; i < 3; ++i) {
         S.eye[i] = (real)V.eye[i];
         S.P[i] = (real)V.P[i];
-        S.bg[i] = (real)V.bg[i];
-        S.amb[i] = (real)V.amb[i];
     }
     S.Lx = (real)V.Lx;
     S.Ly = (real)V.Ly;
     S.medium_index = (real)V.medium_index;
+    S.bg_mat = V.bg_mat;
     return S;
 }
 

@@ -86,7 +86,8 @@ struct SceneView {
     int cam_nx, cam_ny;
     int rec_limit, cull;
     double eye[3], P[3], Lx, Ly;
-    double bg[3], amb[3], medium_index;
+    double medium_index;
+    int bg_mat;   // the background colour: albedo of material slot bg_mat (appended after the scene's)
 };
 
 struct StdParams {

@@ -440,6 +440,17 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         }
         sc.nodes.assign(d.nodes, d.nodes + d.n_nodes);
         sc.mats.assign(d.materials, d.materials + d.n_materials);
+        // device material table: K_a premultiplied by the scene's I_a (the
+        // reference's E_a = mul(m.ambient, scene.ambient), one double product
+        // per channel, shading.cpp:39), and one extra slot whose albedo is the
+        // background colour (DevScene::bg_mat)
+        for (rt_material& m : sc.mats)
+            for (int c = 0; c < 3; ++c) m.ambient[c] = m.ambient[c] * d.ambient[c];
+        {
+            rt_material bgm{};
+            for (int c = 0; c < 3; ++c) bgm.albedo[c] = d.background[c];
+            sc.mats.push_back(bgm);
+        }
         sc.lights.assign(d.lights, d.lights + d.n_lights);
         sc.dlights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
         if (fp32) {
@@ -566,12 +577,11 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     for (int i = 0; i < 3; ++i) {
         S.eye[i] = d.camera.eye[i];
         S.P[i] = d.camera.P[i];
-        S.bg[i] = d.background[i];
-        S.amb[i] = d.ambient[i];
     }
     S.Lx = d.camera.Lx;
     S.Ly = d.camera.Ly;
     S.medium_index = d.medium_index;
+    S.bg_mat = d.n_materials;
 
     if (n_rows > 0 && mode == RT_MODE_STANDARD) {
         // the checkpoint table must reach the last loop row's stream words
