@@ -203,7 +203,9 @@ __device__ __forceinline__ real crosshatch(int band, int x, int y) {
 }
 // material slot: material (>= -3) in the low 24 bits, band in bits 24-27
 __device__ __forceinline__ int paper_mat_pack(int mat, int band) { return (mat & 0xffffff) | (band << 24); }
-__device__ __forceinline__ int paper_mat(int slot) { return (slot << 8) >> 8; }   // (sign-extends the material)
+__device__ __forceinline__ int paper_mat(int slot) {   // (sign-extends the material's 24 bits)
+    return static_cast<int>(static_cast<unsigned>(slot) << 8) >> 8;
+}
 __device__ __forceinline__ int paper_band(int slot) { return (slot >> 24) & 15; }
 
 // Paper-mode primary records: the material slot of a pixel whose ray hit
