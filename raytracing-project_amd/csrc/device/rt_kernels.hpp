@@ -35,8 +35,14 @@ namespace {
 #endif
 constexpr int kStdWPB = RT_STD_WPB;
 constexpr int kStdThreads = 64 * kStdWPB;
-constexpr int kStdBlockX = kStdWPB >= 2 ? 8 : 4;            // pixels per workgroup in x
-constexpr int kStdBlockY = kStdWPB >= 4 ? 4 : 2;            // output rows per workgroup
+// RT_STD_TW: a wave's pixel tile is TW x (8 / TW) pixels (default 4 x 2)
+#ifndef RT_STD_TW
+#define RT_STD_TW 4
+#endif
+constexpr int kStdTW = RT_STD_TW, kStdTH = 8 / RT_STD_TW;
+static_assert(kStdTW * kStdTH == 8, "a wave holds 8 pixels");
+constexpr int kStdBlockX = kStdWPB >= 2 ? 2 * kStdTW : kStdTW;            // pixels per workgroup in x
+constexpr int kStdBlockY = kStdWPB >= 4 ? 2 * kStdTH : kStdTH;            // output rows per workgroup
 
 template <bool C, int NWAVES = 4>
 __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t ni, uint32_t no, Cnt<C>& cnt) {
@@ -101,8 +107,8 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     const int wave = threadIdx.x >> 6;
     const int s = lane & 7;
     const int pix = lane >> 3;
-    const int x = blockIdx.x * kStdBlockX + (wave & 1) * 4 + (pix & 3);
-    const int ri = blockIdx.y * kStdBlockY + (wave >> 1) * 2 + (pix >> 2);
+    const int x = blockIdx.x * kStdBlockX + (wave & 1) * kStdTW + (pix % kStdTW);
+    const int ri = blockIdx.y * kStdBlockY + (wave >> 1) * kStdTH + (pix / kStdTW);
     const bool active = x < P.W && ri < P.n_rows;
     uint32_t ni = 0, no = 0;
     Cnt<C> cnt;
