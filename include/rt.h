@@ -385,13 +385,18 @@ int rt_host_unregister(void* host);
  * checkpoint-table builds / extensions, out[2] first trace-kernel launch
  * (loads the kernels' code object onto the device), out[3] first jitter-fill
  * launch (its code object), out[4] device allocations (hipMalloc), out[5]
- * page-locked host allocations, out[6] stream / event creation.  n <= 7
+ * page-locked host allocations, out[6] stream / event creation; and the
+ * split of the LAST frame (not cumulative): out[7] rt_frame_begin, out[8]
+ * its rt_frame_trace calls, out[9] rt_frame_end, out[10] the device-group
+ * setup of the last rt_render_multi / rt_render_rgb8 call.  min(n, 11)
  * entries are written. */
 int rt_setup_times(double* out, int n);
 /* Release every device resource the library caches (per-device workspaces,
  * resident scenes and jitter tables, the rt_render_multi device groups with
  * their RCCL communicators).  No render may be in flight; later calls
- * re-create what they need.  The `ray` CLI calls it before exit. */
+ * re-create what they need.  The `ray` CLI calls it before exit when it
+ * rendered on several GPUs (RCCL communicators); a one-GPU run leaves the
+ * device memory to process exit. */
 int rt_shutdown(void);
 
 #ifdef __cplusplus

@@ -79,6 +79,11 @@ int rt_test_mt_poly_file(const char* path, int levels);
  *   DESC_FLAGS  it is given flags ^ RT_FLAG_NO_CULL
  *   ABSENT      it does not take part in that frame (a dead peer; the others
  *               time out after run->timeout_ms)
+ *   DESC_SCENE  it renders run->alt_scene instead (another scene content)
+ *   DESC_SHED   its root strip shed (RT_ROOT_SHED_*) is one per mille higher
+ * run->frame_scenes (may be NULL; entries may be NULL): frame fr renders
+ * frame_scenes[fr] instead of s, on the same ranks (a rank handle reused
+ * across scenes).
  * Per frame fr and rank r: run->rc[fr*world + r] (an rt_status, or
  * RT_TEST_RANK_ABSENT), run->ms[...] (the call's wall time), and the error
  * text in run->msgs[(fr*world + r) * msg_cap ...] (may be NULL).  The root's
@@ -91,7 +96,9 @@ enum {
     RT_TEST_FAULT_SETUP = 2,
     RT_TEST_FAULT_DESC_H = 3,
     RT_TEST_FAULT_DESC_FLAGS = 4,
-    RT_TEST_FAULT_ABSENT = 5
+    RT_TEST_FAULT_ABSENT = 5,
+    RT_TEST_FAULT_DESC_SCENE = 6,
+    RT_TEST_FAULT_DESC_SHED = 7
 };
 #define RT_TEST_RANK_ABSENT 1
 typedef struct rt_test_dist_run {
@@ -102,6 +109,8 @@ typedef struct rt_test_dist_run {
     int* rc;
     double* ms;
     char* msgs;
+    const struct rt_scene* const* frame_scenes;
+    const struct rt_scene* alt_scene;
 } rt_test_dist_run;
 int rt_test_dist_threads(const struct rt_scene* s, int W, int H, int mode, int flags, rt_test_dist_run* run,
                          double* fb_host, uint8_t* rgb8_host);

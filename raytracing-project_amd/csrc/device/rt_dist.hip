@@ -113,15 +113,18 @@ int strip_height(int mode) { return mode == RT_MODE_PAPER ? RT_PAPER_STRIP_ROWS 
 // The partition is a pure function of (H, world, mode, kind), all of which
 // the ranks check against each other before the first gather.
 constexpr int kRootShedPaper = 30, kRootShedStd = 8;
-std::vector<int> strip_owners(int n_strips, int world, int mode, int kind) {
+// (RT_ROOT_SHED_PAPER / RT_ROOT_SHED_STD: measurement A/B only.  Both values
+// travel in the frame descriptor, so ranks that see different ones refuse the
+// frame together instead of tracing another partition than the root places.)
+int64_t root_shed(int mode) {
+    static const int shed_paper = [] { const char* e = std::getenv("RT_ROOT_SHED_PAPER"); return e && *e ? std::atoi(e) : kRootShedPaper; }();
+    static const int shed_std = [] { const char* e = std::getenv("RT_ROOT_SHED_STD"); return e && *e ? std::atoi(e) : kRootShedStd; }();
+    return mode == RT_MODE_PAPER ? shed_paper : shed_std;
+}
+std::vector<int> strip_owners(int n_strips, int world, int64_t c) {
     std::vector<int> own((size_t)std::max(0, n_strips), 0);
     if (world <= 1) return own;
     std::vector<int64_t> w((size_t)world, 1000), cur((size_t)world, 0);
-    // (RT_ROOT_SHED_PAPER / RT_ROOT_SHED_STD: measurement A/B only; every rank
-    // of a job must see the same value - the frame descriptor does not carry it)
-    static const int shed_paper = [] { const char* e = std::getenv("RT_ROOT_SHED_PAPER"); return e && *e ? std::atoi(e) : kRootShedPaper; }();
-    static const int shed_std = [] { const char* e = std::getenv("RT_ROOT_SHED_STD"); return e && *e ? std::atoi(e) : kRootShedStd; }();
-    const int64_t c = kind ? 0 : (mode == RT_MODE_PAPER ? shed_paper : shed_std);
     w[0] = std::max<int64_t>(500, 1000 - c * world);
     int64_t total = 0;
     for (int64_t v : w) total += v;
@@ -144,11 +147,13 @@ std::vector<int> strip_owners(int n_strips, int world, int mode, int kind) {
 // wave ticks, exchanged in the trace-status agreement, longest processing
 // time first - was measured and rejected: slower at 2 ranks, no better at 4
 // and 8, profiles/r05_ab/ab_cost_partition.txt.)
-std::vector<std::vector<int32_t>> partition_rows(int H, int world, int mode, int kind) {
+// shed: the root's per-mille shed for this frame (0 for RGB8 output; else
+// root_shed(mode), which every rank checks in the frame descriptor).
+std::vector<std::vector<int32_t>> partition_rows(int H, int world, int mode, int64_t shed) {
     const int S = strip_height(mode);
     const int n_strips = (H + S - 1) / S;
     std::vector<std::vector<int32_t>> rows((size_t)world);
-    const std::vector<int> own = strip_owners(n_strips, world, mode, kind);
+    const std::vector<int> own = strip_owners(n_strips, world, shed);
     for (int st = 0; st < n_strips; ++st)
         for (int r = st * S; r < std::min(H, (st + 1) * S); ++r) rows[own[st]].push_back(r);
     return rows;
@@ -385,7 +390,10 @@ struct rt_dist {
     std::atomic<double> abort_ms{-1.0};       //   its duration once done
     double timeout_ms = 120000.0;             // RT_DIST_TIMEOUT_MS / rt_dist_set_timeout
     int inject = 0;                           // rt_test_dist_inject (next frame only)
-    std::map<const rt_scene*, int64_t> scene_hashes;   // (scenes are immutable)
+    int shed_delta = 0;                       // rt_test_dist_threads fault DESC_SHED (next frame only)
+    // content hashes by rtamd::scene_uid (process-unique, never reused: a scene
+    // loaded after another was destroyed may get its address, never its uid)
+    std::map<uint64_t, int64_t> scene_hashes;
     bool collective() const { return world > 1 || force_collective; }
 };
 
@@ -431,9 +439,11 @@ int dist_init_streams(rt_dist& D, bool coll, bool alt) {
 // asynchronous error; on either the communicator is aborted (ncclCommAbort)
 // and the handle refuses further frames: a rank whose peer died returns
 // RT_ERR_HIP instead of hanging.
-// Descriptor: W, H, mode, output kind, flags and the scene's content hash
-// (ranks that loaded different scenes refuse the frame together).
-constexpr int kDescFields = 6;
+// Descriptor: W, H, mode, output kind, flags, the scene's content hash
+// (ranks that loaded different scenes refuse the frame together) and the
+// root's strip shed of each mode (strip_owners: a rank that saw another
+// RT_ROOT_SHED_* value would trace another partition than the root places).
+constexpr int kDescFields = 8;
 
 // slots: the agreement 1 descriptor (v, -v) + setup status per rank, then the
 // trace status per rank
@@ -641,6 +651,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     const bool coll = D.collective();
     const int inject = D.inject;
     D.inject = 0;
+    const int64_t shed_std = root_shed(RT_MODE_STANDARD) + D.shed_delta, shed_paper = root_shed(RT_MODE_PAPER) + D.shed_delta;
+    D.shed_delta = 0;
     // Local argument checks.  Without a collective they return at once; in a
     // collective frame a failing rank still joins the frame's agreement (below)
     // so that no peer waits for it.
@@ -659,10 +671,11 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     const int S = strip_height(mode == RT_MODE_PAPER ? RT_MODE_PAPER : RT_MODE_STANDARD);
     int64_t shash = 0;   // (the scene's content hash, checked with the descriptor)
     if (s) {
-        auto it = D.scene_hashes.find(s);
+        const uint64_t uid = rtamd::scene_uid(s);
+        auto it = D.scene_hashes.find(uid);
         if (it == D.scene_hashes.end()) {
             if (D.scene_hashes.size() > 64) D.scene_hashes.clear();
-            it = D.scene_hashes.emplace(s, scene_hash(s)).first;
+            it = D.scene_hashes.emplace(uid, scene_hash(s)).first;
         }
         shash = it->second;
     }
@@ -672,7 +685,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         const int rx = dist_init_xchg(D, n_desc + n_stat);
         if (rx != RT_OK) return rx;
     }
-    const std::vector<std::vector<int32_t>> part = partition_rows(Hc, D.world, mode, kind);
+    const std::vector<std::vector<int32_t>> part =
+        partition_rows(Hc, D.world, mode, kind ? 0 : (mode == RT_MODE_PAPER ? shed_paper : shed_std));
     const std::vector<int32_t>& rows = part[D.rank];
     const int n = (int)rows.size();
     int m = 0;
@@ -734,7 +748,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     int64_t* xd = D.xchg.as<int64_t>();
     int64_t* xh = D.xchg_host;
     auto issue_agreement = [&]() -> bool {
-        const int64_t v[kDescFields] = {W, H, mode, kind, flags, shash};
+        const int64_t v[kDescFields] = {W, H, mode, kind, flags, shash, shed_std, shed_paper};
         for (int i = 0; i < kDescFields; ++i) {
             xh[i] = v[i];
             xh[kDescFields + i] = -v[i];
@@ -830,7 +844,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         }
         std::string bad;
         for (int i = 0; i < kDescFields; ++i) {
-            static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags", "scene"};
+            static const char* names[kDescFields] = {"W", "H", "mode", "output kind", "flags", "scene",
+                                                     "RT_ROOT_SHED_STD", "RT_ROOT_SHED_PAPER"};
             if (xh[i] != -xh[kDescFields + i]) bad += std::string(bad.empty() ? "" : ", ") + names[i];
         }
         std::string failed;
@@ -1145,7 +1160,7 @@ extern "C" int rt_dist_rows_mode(int H, int world, int rank, int mode, int32_t* 
     if (H <= 0 || world <= 0 || rank < 0 || rank >= world || !rows_out ||
         (mode != RT_MODE_STANDARD && mode != RT_MODE_PAPER))
         return RT_ERR_INVALID_ARG;
-    const std::vector<int32_t> r = partition_rows(H, world, mode, 0)[rank];
+    const std::vector<int32_t> r = partition_rows(H, world, mode, root_shed(mode))[rank];
     std::copy(r.begin(), r.end(), rows_out);
     return (int)r.size();
 }
@@ -1285,7 +1300,10 @@ extern "C" int rt_test_dist_threads(const rt_scene* s, int W, int H, int mode, i
                     continue;
                 }
                 int Hr = H, fl = flags;
+                const rt_scene* sf = run->frame_scenes && run->frame_scenes[fr] ? run->frame_scenes[fr] : s;
                 if (hit) {
+                    if (run->fault == RT_TEST_FAULT_DESC_SCENE && run->alt_scene) sf = run->alt_scene;
+                    if (run->fault == RT_TEST_FAULT_DESC_SHED) D.shed_delta = 1;
                     if (run->fault == RT_TEST_FAULT_TRACE) D.inject = kInjectTraceFail;
                     if (run->fault == RT_TEST_FAULT_SETUP) D.inject = kInjectSetupFail;
                     if (run->fault == RT_TEST_FAULT_DESC_H) Hr = H + 1;
@@ -1297,7 +1315,7 @@ extern "C" int rt_test_dist_threads(const rt_scene* s, int W, int H, int mode, i
                 }
                 const auto t0 = std::chrono::steady_clock::now();
                 rt_stats stt{};
-                const int rr = dist_frame(D, s, W, Hr, mode, fl, kind, r == 0 ? out.p : nullptr, st, &stt);
+                const int rr = dist_frame(D, sf, W, Hr, mode, fl, kind, r == 0 ? out.p : nullptr, st, &stt);
                 run->ms[o] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 run->rc[o] = rr;
                 if (rr != RT_OK && run->msgs && run->msg_cap > 0)

@@ -30,16 +30,17 @@ def env_ranks() -> tuple[int, int, int]:
 
 def _path(tag: str | None) -> str:
     if tag is None:
-        # port + the common parent (the launcher's agent, or bench.py's own
-        # spawner) + the launcher's run id when it has a real one (torchrun:
+        # port + the launcher's run id when it has a real one (torchrun:
         # TORCHELASTIC_RUN_ID, which static rendezvous leaves at "none";
-        # bench.py: RTAMD_RUN_ID).  The parent pid keeps the name unique per
-        # run, so a file left by a run that died before cleanup() is never
-        # read by the next run's ranks.
+        # bench.py: a unique RTAMD_RUN_ID per run), so ranks started through
+        # their own wrapper processes (a per-rank shell or numactl wrapper,
+        # per-task srun) still meet.  Only without a real run id does the
+        # common parent (the launcher's agent) stand in for it, so a file left
+        # by a run that died before cleanup() is never read by the next run.
         run = os.environ.get("RTAMD_RUN_ID") or os.environ.get("TORCHELASTIC_RUN_ID") or ""
         if run.strip().lower() in ("", "none"):
-            run = "x"
-        tag = f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{run}"
+            run = f"ppid{os.getppid()}"
+        tag = f"{os.environ.get('MASTER_PORT', '0')}_{run}"
     return os.path.join(tempfile.gettempdir(), f"rtamd_uid_{tag}")
 
 

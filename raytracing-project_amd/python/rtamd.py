@@ -506,20 +506,24 @@ class DistRun(C.Structure):
     """rt_test.h rt_test_dist_run."""
     _fields_ = [("world", C.c_int), ("rgb8", C.c_int), ("frames", C.c_int), ("fault_rank", C.c_int),
                 ("fault", C.c_int), ("fault_frame", C.c_int), ("timeout_ms", C.c_int), ("msg_cap", C.c_int),
-                ("rc", C.POINTER(C.c_int)), ("ms", _dp), ("msgs", C.c_char_p)]
+                ("rc", C.POINTER(C.c_int)), ("ms", _dp), ("msgs", C.c_char_p),
+                ("frame_scenes", C.POINTER(C.c_void_p)), ("alt_scene", C.c_void_p)]
 
 
-FAULT_NONE, FAULT_TRACE, FAULT_SETUP, FAULT_DESC_H, FAULT_DESC_FLAGS, FAULT_ABSENT = range(6)
+(FAULT_NONE, FAULT_TRACE, FAULT_SETUP, FAULT_DESC_H, FAULT_DESC_FLAGS, FAULT_ABSENT, FAULT_DESC_SCENE,
+ FAULT_DESC_SHED) = range(8)
 RANK_ABSENT = 1
 
 
 def dist_threads(scene: Scene, width: int, height: int, mode: int, world: int, frames: int = 1,
                  fault: int = FAULT_NONE, fault_rank: int = -1, fault_frame: int = 0, timeout_ms: int = 0,
-                 rgb8: bool = False, flags: int = RT_FLAG_NONE):
+                 rgb8: bool = False, flags: int = RT_FLAG_NONE, frame_scenes=None, alt_scene=None):
     """rt_test_dist_threads: `frames` distributed frames with `world` ranks
     running concurrently on the current device (one host thread, stream set
     and workspace per rank; RCCL replaced by a same-device transport), with an
-    optional fault on one rank in one frame.  Returns (root frames
+    optional fault on one rank in one frame.  frame_scenes: one Scene (or
+    None = `scene`) per frame, rendered in sequence on the same ranks;
+    alt_scene: the scene FAULT_DESC_SCENE gives the faulty rank.  Returns (root frames
     [frames, H, W, 3] - zeros where the root's call failed -, rc [frames,
     world], ms [frames, world], messages [frames][world])."""
     lib = amd_lib()
@@ -530,6 +534,14 @@ def dist_threads(scene: Scene, width: int, height: int, mode: int, world: int, f
     out = np.zeros((frames, height, width, 3), dtype=np.uint8 if rgb8 else np.float64)
     run = DistRun(world, 1 if rgb8 else 0, frames, fault_rank, fault, fault_frame, timeout_ms, cap,
                   rc.ctypes.data_as(C.POINTER(C.c_int)), ms.ctypes.data_as(_dp), C.cast(msgs, C.c_char_p))
+    keep = []
+    if frame_scenes is not None:
+        assert len(frame_scenes) == frames
+        arr = (C.c_void_p * frames)(*[(x.handle.value if x is not None else None) for x in frame_scenes])
+        keep.append(arr)
+        run.frame_scenes = C.cast(arr, C.POINTER(C.c_void_p))
+    if alt_scene is not None:
+        run.alt_scene = alt_scene.handle.value
     if rgb8:
         r = lib.rt_test_dist_threads(scene.handle, width, height, mode, flags, C.byref(run), None,
                                      out.ctypes.data_as(C.POINTER(C.c_uint8)))

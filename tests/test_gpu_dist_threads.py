@@ -19,7 +19,11 @@ for world >= 2, and the timeouts - runs here at world 2, 3 and 8 on config 4
 * a rank failing before its frame begins makes every rank return RT_ERR_HIP,
   the others naming it; the next frame is bit-exact;
 * a rank failing mid-trace (after the agreement) makes every rank return
-  RT_ERR_HIP, the others naming it; the next frame is bit-exact;
+  RT_ERR_HIP, the others naming it "failed while tracing" (frames of >= 2
+  chunks per rank at every world); the next frame is bit-exact;
+* a rank that loaded another scene, or whose root strip shed differs, makes
+  every rank refuse the frame naming "scene" / the shed;
+* one set of ranks renders several scenes in sequence, each bit-exact;
 * a rank that never takes part (a dead peer) makes every other rank give up
   with RT_ERR_HIP within its timeout - no thread outlives it.
 """
@@ -37,7 +41,11 @@ RT_ERR_HIP = -5
 CASES = {
     "cfg4_std": (lambda: scenes.config_json(4, dpi=40)[0], 0),
     "cfg5_paper": (lambda: scenes.config_json(5, dpi=40)[0], 1),
+    # (mid-trace failures: >= 2 row chunks per rank at world 8 needs a rank
+    # owning 2 strips; paper strips are 30 rows, so 360 rows = 12 strips)
+    "cfg5_paper_tall": (lambda: scenes.config_json(5, dpi=160)[0], 1),
 }
+BASE_CASES = ["cfg4_std", "cfg5_paper"]
 WORLDS = [2, 3, 8]
 
 _want_cache = {}
@@ -58,7 +66,7 @@ def _others(world, k):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", BASE_CASES)
 def test_concurrent_ranks_bit_exact(gpu, name, world):
     """Frame after frame (paper frames launch their primary blocks
     costliest first from the second frame on)."""
@@ -74,7 +82,7 @@ def test_concurrent_ranks_bit_exact(gpu, name, world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", BASE_CASES)
 @pytest.mark.parametrize("fault,field", [(4, "flags"), (3, "H")])
 def test_descriptor_mismatch_every_rank_invalid_arg(gpu, name, world, fault, field):
     sc, mode, W, H, want = _case(gpu, name)
@@ -89,7 +97,7 @@ def test_descriptor_mismatch_every_rank_invalid_arg(gpu, name, world, fault, fie
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", BASE_CASES)
 def test_setup_failure_named_by_every_rank(gpu, name, world):
     sc, mode, W, H, want = _case(gpu, name)
     k = world // 2
@@ -104,30 +112,73 @@ def test_setup_failure_named_by_every_rank(gpu, name, world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", ["cfg4_std", "cfg5_paper_tall"])
 def test_mid_frame_trace_failure_then_next_frame_exact(gpu, name, world):
+    """The failure hits the middle of the frame's row chunks (rt_dist.hip
+    chunk_bounds: <= 4, whole strips of the largest share), after the first
+    agreement: every world here has >= 2 chunks, so the verdict always comes
+    from the trace-status agreement."""
     sc, mode, W, H, want = _case(gpu, name)
     k = 0 if world == 2 else world - 2
-    out, rc, ms, msg = gpu.dist_threads(sc, W, H, mode, world, frames=2, fault=gpu.FAULT_TRACE, fault_rank=k)
-    assert (rc[0] == RT_ERR_HIP).all(), (rc[0], msg[0])
-    assert "injected trace failure" in msg[0][k], msg[0][k]
-    # the failure hits the middle of the frame's chunks (rt_dist.hip
-    # chunk_bounds: <= 4, whole strips of the largest share); with a single
-    # chunk that is chunk 0, whose launch the first agreement reports
     rows = (C.c_int32 * H)()
     m = max(gpu.amd_lib().rt_dist_rows_mode(H, world, r, mode, rows) for r in range(world))
     strip = 30 if mode == 1 else 8
-    chunks = min(4, (m + strip - 1) // strip)
-    expect = "failed while tracing" if chunks > 1 else "failed to set up or start the frame"
+    assert min(4, (m + strip - 1) // strip) >= 2, (name, world, m)
+    out, rc, ms, msg = gpu.dist_threads(sc, W, H, mode, world, frames=2, fault=gpu.FAULT_TRACE, fault_rank=k)
+    assert (rc[0] == RT_ERR_HIP).all(), (rc[0], msg[0])
+    assert "injected trace failure" in msg[0][k], msg[0][k]
     for r in _others(world, k):
-        assert f"rank(s) {k} {expect}" in msg[0][r], (chunks, msg[0][r])
+        assert f"rank(s) {k} failed while tracing" in msg[0][r], msg[0][r]
     assert (rc[1] == 0).all(), msg[1]
     assert np.array_equal(out[1], want)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("name", BASE_CASES)
+@pytest.mark.parametrize("fault,field", [("scene", "scene"), ("shed", "RT_ROOT_SHED_STD, RT_ROOT_SHED_PAPER")])
+def test_scene_or_shed_mismatch_every_rank_invalid_arg(gpu, name, world, fault, field):
+    """A rank that loaded another scene (its content hash differs), or whose
+    root strip shed differs (it would trace another partition than the root
+    places), is refused by every rank; the next frame is bit-exact."""
+    sc, mode, W, H, want = _case(gpu, name)
+    k = world - 1
+    if fault == "scene":
+        d = json.loads(CASES[name][0]())
+        d.setdefault("medium", {})["ambient"] = [0.123, 0.123, 0.123]
+        alt = gpu.load_scene_from_json_text(json.dumps(d))
+        out, rc, ms, msg = gpu.dist_threads(sc, W, H, mode, world, frames=2, fault=gpu.FAULT_DESC_SCENE, fault_rank=k,
+                                            alt_scene=alt)
+    else:
+        out, rc, ms, msg = gpu.dist_threads(sc, W, H, mode, world, frames=2, fault=gpu.FAULT_DESC_SHED, fault_rank=k)
+    assert (rc[0] == RT_ERR_INVALID_ARG).all(), (rc[0], msg[0])
+    for r in range(world):
+        assert "disagree on the frame" in msg[0][r] and f"({field})" in msg[0][r], msg[0][r]
+    assert (rc[1] == 0).all(), msg[1]
+    assert np.array_equal(out[1], want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [3])
+def test_same_ranks_render_scenes_in_sequence(gpu, world):
+    """One set of rank handles renders A, B, A, B (a rank's scene cache and
+    content-hash cache reused across scenes): every frame bit-exact."""
+    a, mode, W, H, want_a = _case(gpu, "cfg4_std")
+    d = json.loads(scenes.config_json(4, dpi=40)[0])
+    d.setdefault("medium", {})["ambient"] = [0.3, 0.2, 0.1]
+    b = gpu.load_scene_from_json_text(json.dumps(d))
+    assert (b.width, b.height) == (W, H)
+    want_b = gpu.Tracer(b, W, H, mode).render()
+    assert not np.array_equal(want_a, want_b)
+    out, rc, ms, msg = gpu.dist_threads(a, W, H, mode, world, frames=4, frame_scenes=[a, b, a, b])
+    assert (rc == 0).all(), msg
+    for f, w in enumerate([want_a, want_b, want_a, want_b]):
+        assert np.array_equal(out[f], w), f"frame {f}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", WORLDS)
-@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("name", BASE_CASES)
 def test_absent_rank_every_other_rank_gives_up_in_time(gpu, name, world):
     """A peer that never takes part: every other rank returns RT_ERR_HIP,
     naming the timeout, within its timeout plus its own frame setup (a warm
