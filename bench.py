@@ -102,6 +102,35 @@ def pmc_traffic(config: int, timeout: int = 120) -> dict | None:
     return {"fetch_bytes": fetch, "write_bytes": write, "bytes": fetch + write}
 
 
+SPLIT_NAMES = ["call_ms", "agreement_reduce_ms", "agreement_wait_ms", "gather_ms", "placement_ms",
+               "last_gather_ms", "last_placement_ms", "tail_ms", "rccl_world", "rows"]
+
+
+def ranks_block(kernel_ms: list, rng_ms: list, splits: list) -> dict:
+    """N > 1: every rank's view of its frame, so that an imbalance or a slow
+    collective shows in the driver's own line.  kernel_ms / rng_ms: each
+    rank's mean trace-kernel / jitter time over the timed steps; splits: each
+    rank's rt_dist_frame_split of its last timed frame (include/rt.h)."""
+    world = len(kernel_ms)
+    assert len(splits) == world and len(rng_ms) == world
+    col = {name: [round(float(sp[i]), 4) for sp in splits] for i, name in enumerate(SPLIT_NAMES)}
+    k = [round(float(x), 4) for x in kernel_ms]
+    out = {
+        "kernel_ms": {"min": min(k), "max": max(k), "per_rank": k,
+                      "imbalance": round(max(k) / (sum(k) / world), 4) if sum(k) > 0 else None},
+        "rng_ms": [round(float(x), 4) for x in rng_ms],
+        "rows": [int(x) for x in col["rows"]],
+        "rccl_world": sorted(set(int(x) for x in col["rccl_world"])),
+        "agreement_ms": {"reduce_device": col["agreement_reduce_ms"], "verdict_wait_host": col["agreement_wait_ms"]},
+        "gather_ms": {"per_rank": col["gather_ms"], "last_chunk_per_rank": col["last_gather_ms"]},
+        "placement_ms": {"root_total": col["placement_ms"][0], "root_last_chunk": col["last_placement_ms"][0]},
+        "call_ms": col["call_ms"],
+        "tail_ms": col["tail_ms"],
+        "note": "rt_dist_frame_split of each rank's last timed frame; kernel/rng = means over the timed steps",
+    }
+    return out
+
+
 def host_cpu() -> dict:
     """The CPU the baseline ran on (report nproc and the model)."""
     model = None
@@ -185,8 +214,8 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
                 p.wait()
         for sig, h in old_handlers.items():
             signal.signal(sig, h)
-        try:   # the id file (rendezvous._path: port, the ranks' parent = this process, run id)
-            os.unlink(os.path.join(tempfile.gettempdir(), f"rtamd_uid_{port}_{os.getpid()}_{run_id}"))
+        try:   # the id file (rendezvous._path: port + run id)
+            os.unlink(os.path.join(tempfile.gettempdir(), f"rtamd_uid_{port}_{run_id}"))
         except FileNotFoundError:
             pass
     return rc
@@ -313,9 +342,21 @@ def main() -> int:
     rtamd.device_synchronize()
     elapsed = time.perf_counter() - t0
     k_ms = sum(kernel_ms) / len(kernel_ms)
+    ranks = None
     if world > 1:
         elapsed, k_ms_max = reduce_max([elapsed, k_ms])
         rays_total, traced_total = reduce_sum([rays_local, traced_local])
+        # every rank's split of its last timed frame (after the timed region)
+        sp = (C.c_double * len(SPLIT_NAMES))()
+        if lib.rt_dist_frame_split(dh, sp, len(SPLIT_NAMES)) < 0:
+            raise RuntimeError(f"rt_dist_frame_split failed: {rtamd.last_error()}")
+        mine = [k_ms, sum(rng_ms) / len(rng_ms)] + list(sp)
+        per = len(mine)
+        slots = [-1e300] * (per * world)
+        slots[rank * per:(rank + 1) * per] = mine
+        allv = reduce_max(slots)
+        rows_v = [allv[r * per:(r + 1) * per] for r in range(world)]
+        ranks = ranks_block([v[0] for v in rows_v], [v[1] for v in rows_v], [v[2:] for v in rows_v])
     else:
         k_ms_max, rays_total, traced_total = k_ms, float(rays_local), float(traced_local)
 
@@ -509,6 +550,8 @@ def main() -> int:
         "cpu_baseline": cpu,
         "fp32_fast_path": fp32,
     }
+    if ranks is not None:
+        out["ranks"] = ranks
     print(json.dumps(out), flush=True)
     barrier()
     teardown()

@@ -45,14 +45,16 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5   /* 2: rt_scene_desc gained directional lights
+#define RT_ABI_VERSION 6   /* 2: rt_scene_desc gained directional lights
                               3: rt_stats gained the output-path timings; multi-GPU
                                  and device-output entry points (rt_render_multi,
                                  rt_render_rgb8, rt_dist_*)
                               4: rt_shutdown, device-buffer utilities, rt_dist_reduce_max /
                                  rt_dist_barrier
                               5: rt_dist_set_timeout, per-frame rank agreement,
-                                 rt_host_register / rt_host_unregister */
+                                 rt_host_register / rt_host_unregister
+                              6: rt_dist_frame_split; the frame descriptor carries the
+                                 scene hash and the root strip shed */
 
 /* ---------------------------------------------------------------- errors */
 enum rt_status {
@@ -306,6 +308,18 @@ int rt_dist_barrier(rt_dist* d);
  * timeout is RT_DIST_TIMEOUT_MS from the environment at creation (default
  * 120000) or rt_dist_set_timeout. */
 int rt_dist_set_timeout(rt_dist* d, int timeout_ms);
+/* This rank's split of its last successful collective frame (world > 1, or a
+ * forced-collective world 1), in ms, for diagnosing a multi-GPU run from one
+ * line (bench.py puts every rank's split into its JSON):
+ *   out[0] the whole call (host)        out[1] the frame agreement's reduction (device)
+ *   out[2] host wait for its verdict    out[3] this rank's gathers (device, sum)
+ *   out[4] the root's placements (device, sum; 0 elsewhere)
+ *   out[5] the last chunk's gather      out[6] the last chunk's placement (device)
+ *   out[7] host time from the last enqueue to the call's return
+ *   out[8] the communicator's rank count (ncclCommCount)
+ *   out[9] output rows this rank traced
+ * Writes min(n, 10) entries and returns that count. */
+int rt_dist_frame_split(rt_dist* d, double* out, int n);
 /* The partition of an FP64 frame: writes the output rows of `rank`
  * (ascending) to rows_out (room for H entries) and returns their count; <0
  * on bad arguments.  (RGB8 frames weight every rank equally.)

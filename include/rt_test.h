@@ -111,6 +111,8 @@ typedef struct rt_test_dist_run {
     char* msgs;
     const struct rt_scene* const* frame_scenes;
     const struct rt_scene* alt_scene;
+    double* split;   /* may be NULL: rt_dist_frame_split of rank r after frame fr at
+                        split[(fr*world + r) * 10 ...] (successful frames) */
 } rt_test_dist_run;
 int rt_test_dist_threads(const struct rt_scene* s, int W, int H, int mode, int flags, rt_test_dist_run* run,
                          double* fb_host, uint8_t* rgb8_host);

@@ -149,7 +149,10 @@ int main(int argc, char** argv) {
     // communicators); what is left at exit is the HIP runtime's own teardown
     // of its static state (~40 ms), which the process does not need: leave
     // without the static destructors, as the kernel driver reclaims the rest.
+    // (RT_CLI_NORMAL_EXIT=1: a normal return, for tools that finish their
+    // work in the process's exit handlers, e.g. rocprofv3's trace flush)
     std::cout.flush();
     std::fflush(nullptr);
+    if (const char* e = std::getenv("RT_CLI_NORMAL_EXIT"); e && *e == '1') return 0;
     std::_Exit(0);
 }

@@ -45,7 +45,8 @@
 
 namespace {
 
-constexpr int kChunks = 4;   // pipeline units per rank (chunk k gathered while k+1 is traced)
+constexpr int kChunks = 4;
+constexpr int kSplitSlots = 10;   // rt_dist_frame_split (include/rt.h)   // pipeline units per rank (chunk k gathered while k+1 is traced)
 
 #define HIP_TRY(expr)                                                                            \
     do {                                                                                         \
@@ -367,6 +368,9 @@ struct rt_dist {
     DevBuf mine, mine8, stage, rowtab;
     hipEvent_t ev_chunk[kChunks] = {};
     hipEvent_t ev_gs[kChunks] = {}, ev_ge[kChunks] = {};   // each collective + its placement (comm_st)
+    hipEvent_t ev_gm[kChunks] = {};           // between each collective and its placement (comm_st)
+    hipEvent_t ev_a0 = nullptr, ev_a1 = nullptr;   // around the frame agreement's reduction (comm_st)
+    double split[kSplitSlots] = {};           // rt_dist_frame_split: this rank's last collective frame
     hipEvent_t ev_alt = nullptr;              // end of alt_st's work in a frame (joined into st)
     hipEvent_t ev_tb[2 * kChunks] = {};
     std::vector<int32_t> rowtab_host;          // source of the async row-table upload
@@ -404,15 +408,24 @@ namespace {
 // more than one chunk (a one-GPU frame of the `ray` CLI creates neither: the
 // first stream creations of a process cost ~30 ms of setup,
 // profiles/r05_cli_split.txt).
+int dist_init_events(rt_dist& D) {
+    for (auto& e : D.ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : D.ev_tb) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : D.ev_gs) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : D.ev_gm) HIP_TRY(hipEventCreate(&e));
+    for (auto& e : D.ev_ge) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hipEventCreate(&D.ev_a0));
+    HIP_TRY(hipEventCreate(&D.ev_a1));
+    HIP_TRY(hipEventCreateWithFlags(&D.ev_desc, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
+    return RT_OK;
+}
+
 int dist_init_streams(rt_dist& D, bool coll, bool alt) {
     rtamd::SetupTimer tm(rtamd::kSetupStreams);
     if (!D.ev_alt) {
-        for (auto& e : D.ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (auto& e : D.ev_tb) HIP_TRY(hipEventCreate(&e));
-        for (auto& e : D.ev_gs) HIP_TRY(hipEventCreate(&e));
-        for (auto& e : D.ev_ge) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipEventCreateWithFlags(&D.ev_desc, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&D.ev_alt, hipEventDisableTiming));
+        const int re = dist_init_events(D);
+        if (re != RT_OK) return re;
     }
     if (coll && !D.comm_st) {
         int lo = 0, hi = 0;
@@ -747,6 +760,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     // too.
     int64_t* xd = D.xchg.as<int64_t>();
     int64_t* xh = D.xchg_host;
+    bool a_timed = false;
     auto issue_agreement = [&]() -> bool {
         const int64_t v[kDescFields] = {W, H, mode, kind, flags, shash, shed_std, shed_paper};
         for (int i = 0; i < kDescFields; ++i) {
@@ -758,8 +772,10 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         bool ok = hipMemcpyAsync(xd, xh, n_desc * sizeof(int64_t), hipMemcpyHostToDevice, D.comm_st) == hipSuccess;
         if (!ok) why = "descriptor upload failed";
         if (ok) {
+            a_timed = hipEventRecord(D.ev_a0, D.comm_st) == hipSuccess;
             why = coll_max_i64(D, xd, n_desc, "the frame agreement");
             ok = why.empty();
+            a_timed = a_timed && ok && hipEventRecord(D.ev_a1, D.comm_st) == hipSuccess;
         }
         if (ok) ok = hipMemcpyAsync(xh, xd, n_desc * sizeof(int64_t), hipMemcpyDeviceToHost, D.comm_st) == hipSuccess;
         if (ok && inject == kInjectStall) {
@@ -786,6 +802,8 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     };
     double* fb_rows = direct ? static_cast<double*>(out_root) : D.mine.as<double>();
     int n_tb = 0, n_g = 0;
+    double agree_wait_ms = 0.0;
+    bool gm_ok[kChunks] = {};
     bool status_sent = false, issued = false;
     // Pass 1: every chunk's trace (and toByte) enqueued on its stream and the
     // chunk's end recorded (ev_chunk[k]); agreement 1 issued right after
@@ -837,7 +855,9 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
     }
     if (coll) {
         // (the descriptor reduction ran while the chunks trace)
+        const auto t_aw = std::chrono::steady_clock::now();
         const int rw = dist_wait(D, D.ev_desc, "the frame agreement");
+        agree_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_aw).count();
         if (rw != RT_OK) {
             if (f) (void)rt_frame_end(f, nullptr);
             return rw;
@@ -894,6 +914,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
                     if (D.simg && D.simg->is_aborted(nullptr)) dist_abort(D, why);
                 }
             }
+            gm_ok[n_g] = timed && hipEventRecord(D.ev_gm[n_g], D.comm_st) == hipSuccess;
             if (root) {
                 const int32_t* slots = D.rowtab.as<int32_t>() + (size_t)D.world * a;
                 const hipError_t pe = codes ? place_codes(reinterpret_cast<const uint8_t*>(recv), slots, D.world * (b - a),
@@ -904,6 +925,7 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
             if (timed && hipEventRecord(D.ev_ge[n_g], D.comm_st) == hipSuccess) ++n_g;
         }
     }
+    const auto t_tail = std::chrono::steady_clock::now();
     // alt_st's last work (a chunk's toByte) into st, which rt_frame_end
     // synchronises (without toByte, rt_frame_end joins alt_st's last trace call)
     if (n_tb > 0 && D.alt_st &&
@@ -939,12 +961,37 @@ int dist_frame(rt_dist& D, const rt_scene* s, int W, int H, int mode, int flags,
         for (int i = 0; i < n_g; ++i)
             if (hipEventElapsedTime(&ms, D.ev_gs[i], D.ev_ge[i]) == hipSuccess) g += ms;
         stats->ms_gather = g;
+        if (coll) {
+            // this rank's split of the frame (rt_dist_frame_split)
+            double* sp = D.split;
+            std::fill(sp, sp + kSplitSlots, 0.0);
+            if (a_timed && hipEventElapsedTime(&ms, D.ev_a0, D.ev_a1) == hipSuccess) sp[1] = ms;
+            sp[2] = agree_wait_ms;
+            for (int i = 0; i < n_g; ++i) {
+                float mg = 0.f, mp = 0.f;
+                if (!gm_ok[i] || hipEventElapsedTime(&mg, D.ev_gs[i], D.ev_gm[i]) != hipSuccess ||
+                    hipEventElapsedTime(&mp, D.ev_gm[i], D.ev_ge[i]) != hipSuccess)
+                    continue;
+                sp[3] += mg;
+                sp[4] += mp;
+                if (i == n_g - 1) {
+                    sp[5] = mg;
+                    sp[6] = mp;
+                }
+            }
+            sp[7] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_tail).count();
+            int cw = D.simg ? D.simg->world : D.world;
+            if (D.comm && ncclCommCount(D.comm, &cw) != ncclSuccess) cw = -1;
+            sp[8] = cw;
+            sp[9] = n;
+        }
         double tb = 0.0;
         for (int i = 0; i + 1 < n_tb; i += 2)
             if (hipEventElapsedTime(&ms, D.ev_tb[i], D.ev_tb[i + 1]) == hipSuccess) tb += ms;
         stats->ms_tobyte = tb;
         stats->n_gpus = D.world;
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (coll) D.split[0] = stats->ms_total;
     }
     return RT_OK;
 }
@@ -979,7 +1026,10 @@ void release_rank(rt_dist& d) {
     for (auto& e : d.ev_chunk) drop(e);
     for (auto& e : d.ev_tb) drop(e);
     for (auto& e : d.ev_gs) drop(e);
+    for (auto& e : d.ev_gm) drop(e);
     for (auto& e : d.ev_ge) drop(e);
+    drop(d.ev_a0);
+    drop(d.ev_a1);
     drop(d.ev_alt);
     drop(d.ev_desc);
     (void)hipSetDevice(prev);
@@ -1165,6 +1215,13 @@ extern "C" int rt_dist_rows_mode(int H, int world, int rank, int mode, int32_t* 
     return (int)r.size();
 }
 
+extern "C" int rt_dist_frame_split(rt_dist* d, double* out, int n) {
+    if (!d || !out || n < 0) { rtamd::set_last_error("rt_dist_frame_split: bad arguments"); return RT_ERR_INVALID_ARG; }
+    std::lock_guard<std::mutex> lk(d->mu);
+    for (int i = 0; i < n && i < kSplitSlots; ++i) out[i] = d->split[i];
+    return std::min(n, kSplitSlots);
+}
+
 extern "C" int rt_dist_rows(int H, int world, int rank, int32_t* rows_out) {
     return rt_dist_rows_mode(H, world, rank, RT_MODE_STANDARD, rows_out);
 }
@@ -1318,6 +1375,7 @@ extern "C" int rt_test_dist_threads(const rt_scene* s, int W, int H, int mode, i
                 const int rr = dist_frame(D, sf, W, Hr, mode, fl, kind, r == 0 ? out.p : nullptr, st, &stt);
                 run->ms[o] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 run->rc[o] = rr;
+                if (rr == RT_OK && run->split) std::copy(D.split, D.split + kSplitSlots, run->split + o * kSplitSlots);
                 if (rr != RT_OK && run->msgs && run->msg_cap > 0)
                     std::snprintf(run->msgs + o * run->msg_cap, (size_t)run->msg_cap, "%s", rt_last_error());
                 if (r == 0 && rr == RT_OK) {
@@ -1404,12 +1462,8 @@ extern "C" int rt_test_dist_sim_rank(const rt_scene* s, int W, int H, int mode, 
         if (rs != RT_OK) return rs;
         d->comm_st = streams.comm_st;
         d->alt_st = streams.alt_st;
-        for (auto& e : d->ev_chunk) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (auto& e : d->ev_tb) HIP_TRY(hipEventCreate(&e));
-        for (auto& e : d->ev_gs) HIP_TRY(hipEventCreate(&e));
-        for (auto& e : d->ev_ge) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipEventCreateWithFlags(&d->ev_alt, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&d->ev_desc, hipEventDisableTiming));
+        const int re = dist_init_events(*d);
+        if (re != RT_OK) return re;
     }
     void* o = nullptr;
     if (rank == 0) {

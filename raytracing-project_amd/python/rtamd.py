@@ -183,6 +183,7 @@ def amd_lib():
                                              C.POINTER(C.c_uint8)]
         lib.rt_dist_reduce_max.argtypes = [C.c_void_p, _dp, C.c_int]
         lib.rt_dist_barrier.argtypes = [C.c_void_p]
+        lib.rt_dist_frame_split.argtypes = [C.c_void_p, _dp, C.c_int]
         lib.rt_set_device.argtypes = [C.c_int]
         lib.rt_device_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
         lib.rt_device_free.argtypes = [C.c_void_p]
@@ -507,7 +508,7 @@ class DistRun(C.Structure):
     _fields_ = [("world", C.c_int), ("rgb8", C.c_int), ("frames", C.c_int), ("fault_rank", C.c_int),
                 ("fault", C.c_int), ("fault_frame", C.c_int), ("timeout_ms", C.c_int), ("msg_cap", C.c_int),
                 ("rc", C.POINTER(C.c_int)), ("ms", _dp), ("msgs", C.c_char_p),
-                ("frame_scenes", C.POINTER(C.c_void_p)), ("alt_scene", C.c_void_p)]
+                ("frame_scenes", C.POINTER(C.c_void_p)), ("alt_scene", C.c_void_p), ("split", _dp)]
 
 
 (FAULT_NONE, FAULT_TRACE, FAULT_SETUP, FAULT_DESC_H, FAULT_DESC_FLAGS, FAULT_ABSENT, FAULT_DESC_SCENE,
@@ -517,13 +518,16 @@ RANK_ABSENT = 1
 
 def dist_threads(scene: Scene, width: int, height: int, mode: int, world: int, frames: int = 1,
                  fault: int = FAULT_NONE, fault_rank: int = -1, fault_frame: int = 0, timeout_ms: int = 0,
-                 rgb8: bool = False, flags: int = RT_FLAG_NONE, frame_scenes=None, alt_scene=None):
+                 rgb8: bool = False, flags: int = RT_FLAG_NONE, frame_scenes=None, alt_scene=None,
+                 split_out: np.ndarray | None = None):
     """rt_test_dist_threads: `frames` distributed frames with `world` ranks
     running concurrently on the current device (one host thread, stream set
     and workspace per rank; RCCL replaced by a same-device transport), with an
     optional fault on one rank in one frame.  frame_scenes: one Scene (or
     None = `scene`) per frame, rendered in sequence on the same ranks;
-    alt_scene: the scene FAULT_DESC_SCENE gives the faulty rank.  Returns (root frames
+    alt_scene: the scene FAULT_DESC_SCENE gives the faulty rank; split_out:
+    float64 [frames, world, 10], filled with each rank's rt_dist_frame_split
+    after each successful frame.  Returns (root frames
     [frames, H, W, 3] - zeros where the root's call failed -, rc [frames,
     world], ms [frames, world], messages [frames][world])."""
     lib = amd_lib()
@@ -542,6 +546,9 @@ def dist_threads(scene: Scene, width: int, height: int, mode: int, world: int, f
         run.frame_scenes = C.cast(arr, C.POINTER(C.c_void_p))
     if alt_scene is not None:
         run.alt_scene = alt_scene.handle.value
+    if split_out is not None:
+        assert split_out.shape == (frames, world, 10) and split_out.dtype == np.float64 and split_out.flags.c_contiguous
+        run.split = split_out.ctypes.data_as(_dp)
     if rgb8:
         r = lib.rt_test_dist_threads(scene.handle, width, height, mode, flags, C.byref(run), None,
                                      out.ctypes.data_as(C.POINTER(C.c_uint8)))

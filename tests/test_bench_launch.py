@@ -53,3 +53,58 @@ def test_multi_node_world_is_refused():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], capture_output=True, text=True,
                        timeout=120, env=env, cwd=REPO)
     assert r.returncode != 0 and "LOCAL_WORLD_SIZE" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _check_ranks_block(blk, world, H):
+    assert blk["rccl_world"] == [world]
+    assert len(blk["kernel_ms"]["per_rank"]) == world
+    assert blk["kernel_ms"]["min"] <= blk["kernel_ms"]["max"]
+    assert sum(blk["rows"]) == H
+    for key in ("reduce_device", "verdict_wait_host"):
+        assert len(blk["agreement_ms"][key]) == world
+    assert len(blk["gather_ms"]["per_rank"]) == world and len(blk["gather_ms"]["last_chunk_per_rank"]) == world
+    assert set(blk["placement_ms"]) == {"root_total", "root_last_chunk"}
+    assert len(blk["call_ms"]) == world and len(blk["tail_ms"]) == world
+    json.dumps(blk)   # (goes into the JSON line)
+
+
+def test_ranks_block_schema_synthetic():
+    """The N > 1 line's per-rank block from synthetic rank values (no GPU)."""
+    b = _bench_module()
+    world, H = 3, 50
+    splits = [[1.5 + r, 0.01, 0.02, 0.1, 0.3 if r == 0 else 0.0, 0.03, 0.05 if r == 0 else 0.0, 0.04, world,
+               [18, 16, 16][r]] for r in range(world)]
+    blk = b.ranks_block([1.0, 1.2, 1.1], [0.05] * 3, splits)
+    _check_ranks_block(blk, world, H)
+    assert blk["kernel_ms"]["max"] == 1.2 and blk["placement_ms"]["root_total"] == 0.3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_ranks_block_from_thread_ranks(gpu, world):
+    """The same block from real rank splits: world concurrent ranks on one GPU
+    through the product's dist_frame (rt_test_dist_threads)."""
+    import numpy as np
+
+    import scenes
+
+    b = _bench_module()
+    sc = gpu.load_scene_from_json_text(scenes.config_json(4, dpi=40)[0])
+    W, H = sc.width, sc.height
+    split = np.zeros((2, world, 10))
+    out, rc, ms, msg = gpu.dist_threads(sc, W, H, 0, world, frames=2, split_out=split)
+    assert (rc == 0).all(), msg
+    last = split[1]
+    blk = b.ranks_block([1.0] * world, [0.0] * world, [list(x) for x in last])
+    _check_ranks_block(blk, world, H)
+    assert blk["placement_ms"]["root_total"] > 0 and all(g > 0 for g in blk["gather_ms"]["per_rank"])
+    assert all(c > 0 for c in blk["call_ms"])

@@ -165,7 +165,7 @@ def test_same_ranks_render_scenes_in_sequence(gpu, world):
     content-hash cache reused across scenes): every frame bit-exact."""
     a, mode, W, H, want_a = _case(gpu, "cfg4_std")
     d = json.loads(scenes.config_json(4, dpi=40)[0])
-    d.setdefault("medium", {})["ambient"] = [0.3, 0.2, 0.1]
+    d["background"] = [0.3, 0.2, 0.1]
     b = gpu.load_scene_from_json_text(json.dumps(d))
     assert (b.width, b.height) == (W, H)
     want_b = gpu.Tracer(b, W, H, mode).render()

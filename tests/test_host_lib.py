@@ -32,7 +32,7 @@ def test_libraries_export_every_declared_symbol():
     assert len(declared) >= 18 and "rt_render" in declared and "rt_last_error" in declared
     for name in declared:
         assert hasattr(host, name) or hasattr(amd, name), name
-    assert amd.rt_abi_version() == 5
+    assert amd.rt_abi_version() == 6
 
 
 @pytest.mark.parametrize("H,world", [(2160, 8), (2160, 3), (1080, 2), (17, 4), (5, 8), (1, 1), (4320, 8)])
