@@ -132,6 +132,11 @@ int rt_test_dist_create_rccl1(struct rt_dist** out);
  * rank's timeout (bounded, >= 10 s: the holding kernel always ends), 3 = this
  * rank fails before its frame begins. */
 int rt_test_dist_inject(struct rt_dist* d, int what);
+/* CPU: Pokeball::pick_region_material's acos comparisons as thresholds
+ * (rtamd::pokeball_thresholds, scene_compile.hpp): out2[0] = xb, the least x
+ * in [-1, 1] with acos(x) <= btn_outer (2: none), out2[1] = xi, the greatest
+ * x with acos(x) >= max(0, btn_outer - ring_width) (-2: none).  Returns 0. */
+int rt_test_pokeball_thresholds(double btn_outer, double ring_width, double* out2);
 /* CPU: the paper-mode output code decoder of distributed frames
  * (rtamd::paper_code_value): bits 0-2 edge index in {0, 0.3, 0.5, 0.6, 0.9},
  * bit 3 halved at the frame border, bit 4 the hatch bit (white). */

@@ -1,8 +1,10 @@
 // rt_device.hpp — FP64 device restatement of the reference trace path for
 // gfx950 (CDNA4).  Operation order follows the reference step for step and
 // the file is compiled with -ffp-contract=off and IEEE div/sqrt, so every
-// rounding matches the x86-64 reference except pow() (non-integer exponents)/acos(), which come from
-// the device math library (<= 1 ulp apart).  Citations are
+// rounding matches the x86-64 reference except pow() with a non-integer
+// exponent, which comes from the device math library (<= 1 ulp apart; no
+// reference scene has one).  The pokeball's acos is never evaluated: its two
+// comparisons are thresholds of the host's acos (pick_region).  Citations are
 // raytracer/src/<file>:<line> of the reference.
 //
 // Design:
@@ -447,9 +449,10 @@ __device__ __forceinline__ int pick_region(const NodeT* nd, V3 p, CT& cnt) {
     const real r = v[3];
     const auto uq = div3(p.x - v[0], p.y - v[1], p.z - v[2], r);
     V3 u = v3(uq.x, uq.y, uq.z);
-    const real ang = acos(clamp1(dot3(u, v3(v[7], v[8], v[9]))));
-    const real inner = dmax(RV(0.0), v[5] - v[6]);
-    if (ang <= v[5]) return (ang >= inner) ? nd->mats[RT_PB_RING] : nd->mats[RT_PB_BUTTON];
+    // ang = acos(x) <= btnOuter / ang >= inner as x >= xb / x <= xi: the
+    // thresholds of the host's (the reference's) acos, rtamd::pokeball_thresholds
+    const real x = clamp1(dot3(u, v3(v[7], v[8], v[9])));
+    if (x >= v[rtamd::kPokeXb]) return (x <= v[rtamd::kPokeXi]) ? nd->mats[RT_PB_RING] : nd->mats[RT_PB_BUTTON];
     if (fabs_r(u.y) <= v[4]) return nd->mats[RT_PB_BELT];
     return (u.y >= RV(0.0)) ? nd->mats[RT_PB_TOP] : nd->mats[RT_PB_BOTTOM];
 }

@@ -439,6 +439,8 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
             return RT_ERR_INVALID_ARG;
         }
         sc.nodes.assign(d.nodes, d.nodes + d.n_nodes);
+        for (rt_node& n : sc.nodes)   // pick_region's acos thresholds (device copy only)
+            if (n.kind == RT_NODE_POKEBALL) rtamd::pokeball_thresholds(n.v[5], n.v[6], n.v[rtamd::kPokeXb], n.v[rtamd::kPokeXi]);
         sc.mats.assign(d.materials, d.materials + d.n_materials);
         // device material table: K_a premultiplied by the scene's I_a (the
         // reference's E_a = mul(m.ambient, scene.ambient), one double product

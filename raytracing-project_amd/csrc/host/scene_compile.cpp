@@ -665,9 +665,51 @@ private:
 
 }  // namespace
 
+namespace {
+// doubles of [-1, 1] in order <-> integers (sign-magnitude to two's order)
+int64_t dkey(double x) {
+    int64_t i;
+    std::memcpy(&i, &x, sizeof i);
+    return i >= 0 ? i : -(i & INT64_MAX);
+}
+double dval(int64_t k) {
+    const int64_t i = k >= 0 ? k : ((-k) | INT64_MIN);
+    double x;
+    std::memcpy(&x, &i, sizeof x);
+    return x;
+}
+// least x in [-1, 1] with pred(x), pred monotone (false ... false true ... true)
+template <class P>
+double least_true(P pred) {
+    int64_t lo = dkey(-1.0), hi = dkey(1.0);
+    if (!pred(dval(hi))) return 2.0;
+    if (pred(dval(lo))) return -1.0;
+    while (hi - lo > 1) {   // pred(lo) false, pred(hi) true
+        const int64_t mid = lo + (hi - lo) / 2;
+        (pred(dval(mid)) ? hi : lo) = mid;
+    }
+    return dval(hi);
+}
+}  // namespace
+
+void pokeball_thresholds(double btn_outer, double ring_width, double& xb, double& xi) {
+    const double inner = std::max(0.0, btn_outer - ring_width);
+    xb = least_true([&](double x) { return std::acos(x) <= btn_outer; });
+    // greatest x with acos(x) >= inner = (least x with acos(x) < inner) - 1 ulp
+    const double lt = least_true([&](double x) { return std::acos(x) < inner; });
+    xi = lt == 2.0 ? 1.0 : lt == -1.0 ? -2.0 : dval(dkey(lt) - 1);
+}
+
 CompiledScene compile_scene(const rt_scene_desc& d) {
     Compiler c(d);
     return c.run();
 }
 
 }  // namespace rtamd
+
+// rt_test.h: the pokeball acos thresholds (CPU)
+extern "C" int rt_test_pokeball_thresholds(double btn_outer, double ring_width, double* out2) {
+    if (!out2) return -1;
+    rtamd::pokeball_thresholds(btn_outer, ring_width, out2[0], out2[1]);
+    return 0;
+}

@@ -135,4 +135,18 @@ inline bool accepts_tie(const DevObj& o) {
 // Throws std::runtime_error on malformed IR.
 CompiledScene compile_scene(const rt_scene_desc& d);
 
+// Pokeball::pick_region_material (geometry.cpp:163-180) decides its button /
+// ring regions by comparing ang = std::acos(x), x = clamp1(u . btnDir), with
+// btnOuter and inner = max(0, btnOuter - ringWidth).  The host's acos (glibc,
+// the reference's own) is monotone non-increasing, so
+//   ang <= btnOuter  <=>  x >= xb   (xb: the least double in [-1, 1] with acos(x) <= btnOuter)
+//   ang >= inner     <=>  x <= xi   (xi: the greatest double in [-1, 1] with acos(x) >= inner)
+// and the device compares x with these two thresholds instead of evaluating
+// acos: the reference's decision exactly (the device math library's acos
+// could differ from glibc's in the last bit).  No such x: xb = 2 / xi = -2.
+// Device node slots of a pokeball (rt_render.hip frame_begin fills them in
+// the device copy of the nodes; the IR's v[10..23] of a pokeball are unused).
+constexpr int kPokeXb = 20, kPokeXi = 21;
+void pokeball_thresholds(double btn_outer, double ring_width, double& xb, double& xi);
+
 }  // namespace rtamd
