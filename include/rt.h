@@ -402,8 +402,9 @@ int rt_host_unregister(void* host);
  * page-locked host allocations, out[6] stream / event creation; and the
  * split of the LAST frame (not cumulative): out[7] rt_frame_begin, out[8]
  * its rt_frame_trace calls, out[9] rt_frame_end, out[10] the device-group
- * setup of the last rt_render_multi / rt_render_rgb8 call.  min(n, 11)
- * entries are written. */
+ * setup of the last rt_render_multi / rt_render_rgb8 call; out[11] the
+ * one-time copy-engine warm-up (host time, overlapped with the first
+ * frame's trace).  min(n, 12) entries are written. */
 int rt_setup_times(double* out, int n);
 /* Release every device resource the library caches (per-device workspaces,
  * resident scenes and jitter tables, the rt_render_multi device groups with

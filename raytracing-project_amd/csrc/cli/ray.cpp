@@ -122,8 +122,8 @@ int main(int argc, char** argv) {
         auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
         const double ms_render = ms(t0, t1);
         const double rays = (double)(s.rays_intersect + s.rays_occluded);
-        double setup[11] = {};
-        (void)rt_setup_times(setup, 11);
+        double setup[12] = {};
+        (void)rt_setup_times(setup, 12);
         // ms_render's host split, in order: output-buffer prefault join,
         // rt_render_rgb8's group setup, rt_frame_begin (scene compile + upload,
         // jitter checkpoint table, jitter launch), the trace launches,
@@ -133,9 +133,9 @@ int main(int argc, char** argv) {
             "\"ms_setup_trace_load\": %.3f, \"ms_setup_jitter_load\": %.3f, \"ms_setup_alloc\": %.3f, "
             "\"ms_setup_pinned\": %.3f, \"ms_setup_streams\": %.3f, \"ms_prefault_join\": %.3f, "
             "\"ms_group\": %.3f, \"ms_frame_begin\": %.3f, \"ms_frame_trace\": %.3f, \"ms_frame_end\": %.3f, "
-            "\"ms_shutdown\": %.3f}\n",
+            "\"ms_setup_copy_engine\": %.3f, \"ms_shutdown\": %.3f}\n",
             ms(t_hip0, t_hip1), setup[0], setup[1], setup[2], setup[3], setup[4], setup[5], setup[6],
-            ms(t0, t_joined), setup[10], setup[7], setup[8], setup[9], ms(t2, t3));
+            ms(t0, t_joined), setup[10], setup[7], setup[8], setup[9], setup[11], ms(t2, t3));
         std::printf(
             "{\"rays_intersect\": %llu, \"rays_occluded\": %llu, \"rays_traced\": %llu, \"n_gpus\": %d, "
             "\"ms_load\": %.3f, \"ms_rng\": %.3f, \"ms_kernel\": %.3f, \"ms_gather\": %.3f, \"ms_tobyte\": %.3f, "

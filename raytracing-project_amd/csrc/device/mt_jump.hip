@@ -396,7 +396,7 @@ hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
     if (levels > MAX_LEVELS) return hipErrorInvalidValue;
     hipError_t e = hipSuccess;
     if (plan.K != kTableK || plan.levels < levels) {
-        e = plan.build(kTableK, levels);
+        e = plan.build(kTableK, levels, stream);
         if (e != hipSuccess) return e;
     }
     // The coarse checkpoints (every R-th table entry: c = R*c') by the jump
@@ -416,14 +416,22 @@ hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
     uint32_t* d_ckpt = nullptr;
     int64_t* d_list = nullptr;
     uint32_t* d_tab = nullptr;
+    int64_t* h_list = nullptr;   // page-locked staging of the lists (host_copy_async)
     hipEvent_t e0 = nullptr, e1 = nullptr;
     e = hipMalloc(&d_ckpt, (size_t)n_coarse * kMTParts * N * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&d_list, std::max<size_t>(1, lists.size()) * sizeof(int64_t));
     if (e == hipSuccess) e = hipMalloc(&d_tab, (size_t)n_new * N * sizeof(uint32_t));
     if (e == hipSuccess) e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
-    if (e == hipSuccess && !lists.empty())
-        e = hipMemcpyAsync(d_list, lists.data(), lists.size() * sizeof(int64_t), hipMemcpyHostToDevice, stream);
+    if (e == hipSuccess && !lists.empty()) {
+        e = hipHostMalloc(reinterpret_cast<void**>(&h_list), lists.size() * sizeof(int64_t), hipHostMallocDefault);
+        if (e == hipSuccess) {
+            std::copy(lists.begin(), lists.end(), h_list);
+            e = host_copy_async(d_list, h_list, lists.size() * sizeof(int64_t), stream);
+        } else {
+            h_list = nullptr;
+        }
+    }
     if (e == hipSuccess) e = hipEventRecord(e0, stream);
     if (e == hipSuccess) e = hipMemcpyAsync(d_ckpt, plan.d_base, N * sizeof(uint32_t), hipMemcpyDeviceToDevice, stream);
     int8_t parts[MAX_LEVELS] = {1, 1, 1, 1, 1, 1, 1, 1};
@@ -454,6 +462,9 @@ hipError_t JitterTable::ensure(int64_t n_need, hipStream_t stream) {
     }
     if (e == hipSuccess) e = hipEventRecord(e1, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    else (void)hipStreamSynchronize(stream);   // (nothing queued may read what is freed below)
+    plan.drop_stage();
+    if (h_list) (void)hipHostFree(h_list);
     if (e == hipSuccess) (void)hipEventElapsedTime(&ms_last_build, e0, e1);
     if (d_ckpt) (void)hipFree(d_ckpt);
     if (d_list) (void)hipFree(d_list);
@@ -526,17 +537,26 @@ static void locate_poly_file() {
     });
 }
 
-hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
+hipError_t JitterPlan::build(int K_blocks, int levels_needed, hipStream_t stream) {
     release();
     locate_poly_file();
     std::vector<uint32_t> polys = mt_tree_polys(K_blocks, levels_needed);
     // the set coefficients of every polynomial, in order (~2.3 M taps for 4
     // levels): sized by popcount, then one ctz walk per word (a bit-by-bit
-    // scan took ~40 ms of the CLI's one-time setup)
+    // scan took ~40 ms of the CLI's one-time setup), written straight into
+    // the page-locked staging: [seed window | taps]
     const size_t n_poly = (size_t)levels_needed * (kMTRadix - 1);
     size_t n_taps = 0;
     for (size_t k = 0; k < n_poly * kPolyWords32; ++k) n_taps += (size_t)__builtin_popcount(polys[k]);
-    std::vector<uint16_t> taps(n_taps + 8, 0);
+    const size_t win_bytes = (size_t)N * sizeof(uint32_t);
+    const size_t taps_cap = n_taps + 8;
+    hipError_t e = hipHostMalloc(&h_stage, win_bytes + taps_cap * sizeof(uint16_t), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        h_stage = nullptr;
+        return e;
+    }
+    uint32_t* win = static_cast<uint32_t*>(h_stage);
+    uint16_t* taps = reinterpret_cast<uint16_t*>(static_cast<char*>(h_stage) + win_bytes);
     size_t o = 0;
     off.assign(1, 0);
     for (int j = 0; j < levels_needed; ++j)
@@ -551,14 +571,15 @@ hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
             }
             off.push_back((int32_t)o);
         }
-    taps.resize(o + 8, 0);
-    uint32_t win[kMTN];
+    for (int k = 0; k < 8; ++k) taps[o + k] = 0;
+    const size_t n_up = o + 8;
     mt_first_window(12345u, win);
-    hipError_t e = hipMalloc(&d_taps, taps.size() * sizeof(uint16_t));
-    if (e == hipSuccess) e = hipMalloc(&d_base, sizeof(win));
-    if (e == hipSuccess) e = hipMemcpy(d_taps, taps.data(), taps.size() * sizeof(uint16_t), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_base, win, sizeof(win), hipMemcpyHostToDevice);
+    e = hipMalloc(&d_taps, n_up * sizeof(uint16_t));
+    if (e == hipSuccess) e = hipMalloc(&d_base, win_bytes);
+    if (e == hipSuccess) e = host_copy_async(d_taps, taps, n_up * sizeof(uint16_t), stream);
+    if (e == hipSuccess) e = host_copy_async(d_base, win, win_bytes, stream);
     if (e != hipSuccess) {
+        (void)hipStreamSynchronize(stream);
         release();
         return e;
     }
@@ -567,7 +588,13 @@ hipError_t JitterPlan::build(int K_blocks, int levels_needed) {
     return hipSuccess;
 }
 
+void JitterPlan::drop_stage() {
+    if (h_stage) (void)hipHostFree(h_stage);
+    h_stage = nullptr;
+}
+
 void JitterPlan::release() {
+    drop_stage();
     if (d_taps) (void)hipFree(d_taps);
     if (d_base) (void)hipFree(d_base);
     d_taps = nullptr;

@@ -23,7 +23,13 @@ struct JitterPlan {
     uint16_t* d_taps = nullptr;
     uint32_t* d_base = nullptr;        // window at n = 624 for seed 12345
     std::vector<int32_t> off;          // taps of (j, m) at [off[j*R+m], off[j*R+m+1]), m in 1..R-1
-    hipError_t build(int K_blocks, int levels_needed);   // synchronous upload
+    // Uploads the taps and the seed window on `stream` from page-locked
+    // staging (h_stage: freed by drop_stage() once the stream has passed the
+    // copies).  A pageable synchronous copy of the ~4.6 MB of taps took ~7.6
+    // ms of the CLI's one-time setup (profiles/r06c_cli_prof.txt).
+    hipError_t build(int K_blocks, int levels_needed, hipStream_t stream);
+    void* h_stage = nullptr;
+    void drop_stage();
     void release();
 };
 

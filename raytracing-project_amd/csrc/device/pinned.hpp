@@ -63,11 +63,26 @@ struct PinnedArena {
     }
 };
 
-// hipMemcpyAsync H2D through the arena (pageable source if it has no room).
+// dst[0, n) <- page-locked src[0, n) by a kernel on st (k_host_copy,
+// rt_render.hip: the GPU reads the host memory over PCIe).  Both pointers
+// 16-byte aligned, else hipMemcpyAsync.  A process's first copy-engine
+// transfer costs ~8 ms of host time in the runtime (profiles/
+// r06d_first_op.txt: pageable or page-locked alike; a kernel's own first
+// launch ~0.3 ms), so a frame's uploads never use the copy engines.
+hipError_t host_copy_async(void* dst, const void* src_pinned, size_t n, hipStream_t st);
+// Once per process: a 16-byte device-to-host copy-engine transfer on st, so
+// that the runtime's one-time copy-engine setup (host time in the call)
+// runs while the frame's kernels execute instead of in front of the
+// frame's read-back.
+hipError_t warm_copy_engine(hipStream_t st);
+
+// H2D through the arena: page-locked staging + k_host_copy (pageable
+// hipMemcpyAsync if the arena has no room).
 inline hipError_t upload_async(PinnedArena* a, void* dst, const void* src, size_t n, hipStream_t st) {
     if (!n) return hipSuccess;
     const void* s = a ? a->put(src, n) : nullptr;
-    return hipMemcpyAsync(dst, s ? s : src, n, hipMemcpyHostToDevice, st);
+    if (s) return host_copy_async(dst, s, n, st);
+    return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
 }
 
 // Wait for an event by polling it (yielding the core between polls; after

@@ -541,7 +541,7 @@ void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const 
 
 // Eager scenes always use D.  Each variant gets its own register allocation.
 void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneView& V, const StdParams& P) {
-    const bool bv = !e && !d && V.cull && V.n_bounded >= 4 && V.n_chunks > 0;
+    const bool bv = !e && !d && V.wave_cull && V.n_chunks > 0;
     const DevScene S = make_scene(V, bv);
     const dim3 grid((P.W + kStdBlockX - 1) / kStdBlockX, (P.n_rows + kStdBlockY - 1) / kStdBlockY);
 #ifdef RT_GENERAL_ONLY
@@ -551,7 +551,7 @@ void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneVie
     if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
     else launch_std_c<true, true, false>(c, grid, st, S, P);
 #else
-    const bool wv = V.cull && V.n_bounded >= 4;
+    const bool wv = V.wave_cull;
     if (e) {
         if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
         else launch_std_c<true, true, false>(c, grid, st, S, P);
@@ -584,14 +584,14 @@ void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneVie
 }
 
 void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const SceneView& V, const PaperParams& P) {
-    const bool bv = !e && !d && V.cull && V.n_bounded >= 4 && V.n_chunks > 0;
+    const bool bv = !e && !d && V.wave_cull && V.n_chunks > 0;
     const DevScene S = make_scene(V, bv);
 #ifdef RT_GENERAL_ONLY
     (void)e;
     (void)d;
     launch_paper_c<true, true>(c, grid, st, S, P);
 #else
-    const bool wv = V.cull && V.n_bounded >= 4;
+    const bool wv = V.wave_cull;
     if (e) launch_paper_c<true, true>(c, grid, st, S, P);
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
     else if (bv) {

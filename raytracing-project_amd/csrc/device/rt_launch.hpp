@@ -83,6 +83,7 @@ struct SceneView {
     int n_wobjs, n_chunks;
     int n_lights, n_dlights, n_objs;
     int n_bounded;
+    int wave_cull;   // wave-level culls: cull && n_bounded >= wave_cull_min() (host-decided)
     int cam_nx, cam_ny;
     int rec_limit, cull;
     double eye[3], P[3], Lx, Ly;
@@ -154,6 +155,10 @@ constexpr int kMaxDepth = 16;     // reflection/refraction frames (medium.recurs
 constexpr int kBigRayStack = 64;
 constexpr int kBigIvlSpill = 62;
 constexpr int kBigDepth = 128;    // medium.recursion <= 129
+
+// Scenes with at least this many bounded objects take the wave-level culling
+// kernels (WV >= 1).  RT_WV_MIN overrides it (measurement A/B; default 4).
+int wave_cull_min();
 
 constexpr int kCounterWords = 2 + 16;   // isect, occl, ops[16]
 constexpr int kCounterSlots = 512;      // spread of the per-block counter atomics

@@ -421,8 +421,10 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     Workspace& ws = *f->ws;
     const bool fp32 = (flags & RT_FLAG_FP32) != 0;
     SceneCache& sc = ws.sc;
+    ws.up.reset();   // (the previous frame's uploads completed: its rt_frame_end synchronised)
     if (!sc.valid || sc.uid != rtamd::scene_uid(s) || sc.fp32 != fp32) {
         // compile + upload the scene once; later frames of it find it resident
+        // (uploads from the page-locked arena: plain DMA, no pageable staging)
         const auto t_sc = SClock::now();
         struct AddTime {
             SClock::time_point t;
@@ -457,29 +459,29 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         sc.dlights.assign(d.dir_lights, d.dir_lights + d.n_dir_lights);
         if (fp32) {
             make_float_scene(sc);
-            HIP_TRY(upload(ws.nodes_f, sc.nodes_f, st));
-            HIP_TRY(upload(ws.mats_f, sc.mats_f, st));
-            HIP_TRY(upload(ws.lights_f, sc.lights_f, st));
-            HIP_TRY(upload(ws.dlights_f, sc.dlights_f, st));
-            HIP_TRY(upload(ws.fold_f, sc.fold_f, st));
+            HIP_TRY(upload(ws.nodes_f, sc.nodes_f, st, &ws.up));
+            HIP_TRY(upload(ws.mats_f, sc.mats_f, st, &ws.up));
+            HIP_TRY(upload(ws.lights_f, sc.lights_f, st, &ws.up));
+            HIP_TRY(upload(ws.dlights_f, sc.dlights_f, st, &ws.up));
+            HIP_TRY(upload(ws.fold_f, sc.fold_f, st, &ws.up));
         } else {
-            HIP_TRY(upload(ws.nodes, sc.nodes, st));
-            HIP_TRY(upload(ws.mats, sc.mats, st));
-            HIP_TRY(upload(ws.lights, sc.lights, st));
-            HIP_TRY(upload(ws.dlights, sc.dlights, st));
-            HIP_TRY(upload(ws.fold, sc.cs.fold, st));
+            HIP_TRY(upload(ws.nodes, sc.nodes, st, &ws.up));
+            HIP_TRY(upload(ws.mats, sc.mats, st, &ws.up));
+            HIP_TRY(upload(ws.lights, sc.lights, st, &ws.up));
+            HIP_TRY(upload(ws.dlights, sc.dlights, st, &ws.up));
+            HIP_TRY(upload(ws.fold, sc.cs.fold, st, &ws.up));
         }
-        HIP_TRY(upload(ws.objs, sc.cs.objs, st));
-        HIP_TRY(upload(ws.ops, sc.cs.ops, st));
-        HIP_TRY(upload(ws.gb, sc.cs.gbounds, st));
-        HIP_TRY(upload(ws.ctab, sc.cs.ctab, st));
-        HIP_TRY(upload(ws.lrec, sc.cs.lrec, st));
-        HIP_TRY(upload(ws.lwrec, sc.cs.lwrec, st));
-        HIP_TRY(upload(ws.lgb, sc.cs.lgb, st));
-        HIP_TRY(upload(ws.wobjs, sc.cs.wobjs, st));
-        HIP_TRY(upload(ws.wctab, sc.cs.wctab, st));
-        HIP_TRY(upload(ws.worig, sc.cs.worig, st));
-        HIP_TRY(upload(ws.wchunk, sc.cs.wchunk, st));
+        HIP_TRY(upload(ws.objs, sc.cs.objs, st, &ws.up));
+        HIP_TRY(upload(ws.ops, sc.cs.ops, st, &ws.up));
+        HIP_TRY(upload(ws.gb, sc.cs.gbounds, st, &ws.up));
+        HIP_TRY(upload(ws.ctab, sc.cs.ctab, st, &ws.up));
+        HIP_TRY(upload(ws.lrec, sc.cs.lrec, st, &ws.up));
+        HIP_TRY(upload(ws.lwrec, sc.cs.lwrec, st, &ws.up));
+        HIP_TRY(upload(ws.lgb, sc.cs.lgb, st, &ws.up));
+        HIP_TRY(upload(ws.wobjs, sc.cs.wobjs, st, &ws.up));
+        HIP_TRY(upload(ws.wctab, sc.cs.wctab, st, &ws.up));
+        HIP_TRY(upload(ws.worig, sc.cs.worig, st, &ws.up));
+        HIP_TRY(upload(ws.wchunk, sc.cs.wchunk, st, &ws.up));
         sc.uid = rtamd::scene_uid(s);
         sc.fp32 = fp32;
         sc.valid = true;
@@ -533,7 +535,6 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
     HIP_TRY(ws.counters.ensure(ctr_bytes));
     HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
-    ws.up.reset();   // (the previous frame's uploads completed: its rt_frame_end synchronised)
 
     SceneView& S = f->S;
     S.nodes = fp32 ? ws.nodes_f.p : ws.nodes.p;
@@ -576,6 +577,7 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.cam_ny = rt_camera_height(&d.camera);
     S.rec_limit = d.recursion_limit;
     S.cull = (flags & RT_FLAG_NO_CULL) ? 0 : 1;
+    S.wave_cull = S.cull && S.n_bounded >= rtamd::wave_cull_min();
     for (int i = 0; i < 3; ++i) {
         S.eye[i] = d.camera.eye[i];
         S.P[i] = d.camera.P[i];
@@ -867,6 +869,7 @@ int frame_trace(rt_frame* f, int ri0, int ri1, double* fb, hipStream_t hs, uint8
     }
     HIP_TRY(hipEventRecord(ws.tev[f->n_tev], st));
     rtamd::note_setup_ms(rtamd::kLastTrace, ms_since(t_launch));
+    HIP_TRY(rtamd::warm_copy_engine(st));   // (once per process, while the trace runs)
     unmark.keep = true;
     f->call_st.push_back(st);
     ++f->n_tev;
@@ -993,10 +996,53 @@ int render_rows_impl(const rt_scene* s, int W, int H, int mode, int flags, const
 
 void rtamd::set_workspace_slot(int slot) { t_ws_slot = slot; }
 
+namespace {
+// dst <- page-locked host src, 16-byte words (+ a byte tail), read by the GPU over PCIe
+__global__ void k_host_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16, int tail) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail)
+        reinterpret_cast<unsigned char*>(dst + n16)[threadIdx.x] = reinterpret_cast<const unsigned char*>(src + n16)[threadIdx.x];
+}
+}  // namespace
+
+hipError_t rtamd::host_copy_async(void* dst, const void* src, size_t n, hipStream_t st) {
+    if (!n) return hipSuccess;
+    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
+        return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+    const size_t n16 = n / 16;
+    const int tail = (int)(n - n16 * 16);
+    const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(1024, (n16 + 255) / 256));
+    hipLaunchKernelGGL(k_host_copy, dim3(blocks), dim3(256), 0, st, static_cast<const uint4*>(src),
+                       static_cast<uint4*>(dst), n16, tail);
+    return hipGetLastError();
+}
+
+hipError_t rtamd::warm_copy_engine(hipStream_t st) {
+    static std::mutex mu;
+    static bool done = false;
+    static void* dev = nullptr;
+    static void* host = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done) return hipSuccess;
+    done = true;   // (one attempt: the copy is an optimisation only)
+    rtamd::SetupTimer tm(rtamd::kSetupCopyEngine);
+    if (hipMalloc(&dev, 16) != hipSuccess || hipHostMalloc(&host, 16, hipHostMallocDefault) != hipSuccess) return hipSuccess;
+    return hipMemcpyAsync(host, dev, 16, hipMemcpyDeviceToHost, st);
+}
+
+int rtamd::wave_cull_min() {
+    static const int v = [] {
+        const char* e = std::getenv("RT_WV_MIN");
+        return e && *e ? std::max(1, std::atoi(e)) : 4;
+    }();
+    return v;
+}
+
 void rtamd::note_setup_ms(int slot, double ms) {
     if (slot < 4 || slot >= kSetupSlots) return;
     std::lock_guard<std::mutex> lk(g_setup.mu);
-    if (slot < kLastBegin || slot == kLastTrace) g_setup.extra[slot] += ms;
+    if (slot < kLastBegin || slot == kLastTrace || slot == kSetupCopyEngine) g_setup.extra[slot] += ms;
     else g_setup.extra[slot] = ms;
 }
 
@@ -1314,7 +1360,7 @@ extern "C" int rt_test_jitter_device(int K, int64_t q0, int64_t q1, int64_t firs
         return RT_OK;
     }
     rtamd::JitterPlan plan;
-    HIP_TRY(plan.build(K, rtamd::mt_levels_needed(K, q1)));
+    HIP_TRY(plan.build(K, rtamd::mt_levels_needed(K, q1), nullptr));
     DBuf dc, dj, ds;
     const std::vector<rtamd::JRange> ranges{rtamd::JRange{q0, q1, 0}};
     rtamd::JitterJob job;
@@ -1347,7 +1393,7 @@ extern "C" int rt_test_kernel_name(const rt_scene* s, int mode, int flags, char*
         for (const auto& o : cs.objs)
             if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
         const bool f32 = (flags & RT_FLAG_FP32) != 0;
-        const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
+        const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= rtamd::wave_cull_min();
         const bool bv = wv && !cs.wchunk.empty() && !(flags & RT_FLAG_NO_BVH);
         const bool cnt = (flags & RT_FLAG_COUNT_OPS) != 0;
         const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
@@ -1392,7 +1438,7 @@ extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32
         int n_bounded = 0;
         for (const auto& o : cs.objs)
             if (o.has_bound && o.kind != rtamd::OBJ_GROUP) ++n_bounded;
-        const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= 4;
+        const bool wv = !(flags & RT_FLAG_NO_CULL) && n_bounded >= rtamd::wave_cull_min();
         const bool bv = wv && !cs.has_eager && !deep && !cs.wchunk.empty() && !(flags & RT_FLAG_NO_BVH);
         const bool f32 = (flags & RT_FLAG_FP32) != 0;
         const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;

@@ -34,7 +34,7 @@ int paper_chunks_1gpu();
 // its frame: device group, output buffer).
 enum {
     kSetupAlloc = 4, kSetupPinned = 5, kSetupStreams = 6,
-    kLastBegin = 7, kLastTrace = 8, kLastEnd = 9, kLastGroup = 10, kSetupSlots = 11
+    kLastBegin = 7, kLastTrace = 8, kLastEnd = 9, kLastGroup = 10, kSetupCopyEngine = 11, kSetupSlots = 12
 };
 void note_setup_ms(int slot, double ms);   // slots 4..6: add; 7..10: set (kLastTrace adds within a frame)
 struct SetupTimer {
