@@ -2466,21 +2466,22 @@ __device__ __forceinline__ double pow_spec(double x, double y) {
     const int k = (int)y;
     if (!(y >= 0.0 && y < 1024.0 && (double)k == y)) return pow_general(x, y);
     if (k == 0) return 1.0;   // pow(x, 0) = 1 for every x
+    // (h, l): an unnormalised double-double (h the rounded product, l the
+    // exact product error by fma plus the cross term), 4 / 3 operations per
+    // squaring / multiplication instead of 7 with renormalisation.  Equal bit
+    // for bit to the renormalised evaluation except below 2^-1000, where the
+    // specular term is 0 to far beyond any tolerance (50 M random (x, k),
+    // tools/probe/pow_dd_check.c).
     const int top = 31 - __builtin_clz(k);
     double h = x, l = 0.0;
     for (int i = top - 1; i >= 0; --i) {
-        // (h, l)^2
-        double p = h * h;
-        double e = __builtin_fma(h, h, -p);
-        e = e + (2.0 * h) * l;
-        h = p + e;
-        l = e - (h - p);
+        double p = h * h;   // (h, l)^2
+        l = __builtin_fma(h + h, l, __builtin_fma(h, h, -p));
+        h = p;
         if ((k >> i) & 1) {   // (h, l) * x
             p = h * x;
-            e = __builtin_fma(h, x, -p);
-            e = e + l * x;
-            h = p + e;
-            l = e - (h - p);
+            l = __builtin_fma(l, x, __builtin_fma(h, x, -p));
+            h = p;
         }
     }
     return h + l;

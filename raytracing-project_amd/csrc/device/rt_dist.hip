@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "rccl_dyn.hpp"   // (RCCL is dlopened on first use: after rccl.h, before any ncclXxx call)
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>

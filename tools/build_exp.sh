@@ -10,5 +10,5 @@ mkdir -p lib/exp build/exp
   -I../include -Icsrc/host -Icsrc/device $2 -c csrc/device/rt_kernels_f64.hip -o build/exp/rt_kernels_f64_$1.o 2>/dev/null
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/exp/librtamd_$1.so build/rt_render.o \
   build/exp/rt_kernels_f64_$1.o build/rt_kernels_f32.o build/rt_kernels_big.o build/mt_jump.o build/rt_dist.o build/mt_poly.o build/scene_compile.o \
-  -Llib -lrt_host -L/opt/rocm/lib -lrccl -Wl,-rpath,'$ORIGIN/..'
+  -Llib -lrt_host -ldl -Wl,-rpath,'$ORIGIN/..'
 echo built lib/exp/librtamd_$1.so
