@@ -53,8 +53,8 @@ extern "C" {
                                  rt_dist_barrier
                               5: rt_dist_set_timeout, per-frame rank agreement,
                                  rt_host_register / rt_host_unregister
-                              6: rt_dist_frame_split; the frame descriptor carries the
-                                 scene hash and the root strip shed */
+                              6: rt_dist_frame_split, rt_warmup; the frame descriptor
+                                 carries the scene hash and the root strip shed */
 
 /* ---------------------------------------------------------------- errors */
 enum rt_status {
@@ -406,6 +406,15 @@ int rt_host_unregister(void* host);
  * one-time copy-engine warm-up (host time, overlapped with the first
  * frame's trace).  min(n, 12) entries are written. */
 int rt_setup_times(double* out, int n);
+/* One-time preparation a caller can start early, e.g. on a helper thread
+ * while its main thread initialises HIP or parses the scene:
+ *   RT_WARM_HOST    host-only: the jitter stream's jump-tree tap lists (read
+ *                   from lib/mt19937_tree.polys; ~3 ms), cached for the process
+ *   RT_WARM_DEVICE  loads the FP64 render kernels' code object onto the
+ *                   current device (~5 ms at a process's first trace launch)
+ * Thread-safe; the frames that follow find the work done. */
+enum { RT_WARM_HOST = 1, RT_WARM_DEVICE = 2 };
+int rt_warmup(int what);
 /* Release every device resource the library caches (per-device workspaces,
  * resident scenes and jitter tables, the rt_render_multi device groups with
  * their RCCL communicators).  No render may be in flight; later calls

@@ -46,6 +46,15 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--gpus") && i + 1 < argc) n_gpus = std::atoi(argv[++i]);
     }
 
+    // one-time host preparation (the jitter tree's tap lists, ~3 ms) on a
+    // helper thread while this one loads the scene and initialises HIP
+    std::thread warm_host([] { (void)rt_warmup(RT_WARM_HOST); });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } join_host{warm_host};
     rtamd::Scene scene;
     rtamd::Camera cam;
     try {
@@ -90,6 +99,10 @@ int main(int argc, char** argv) {
     const auto t_hip0 = std::chrono::steady_clock::now();
     (void)rt_device_count();
     const auto t_hip1 = std::chrono::steady_clock::now();
+    // the render kernels' code object (~5 ms) loads on a helper thread while
+    // this one compiles and uploads the scene and builds the jitter table
+    std::thread warm_dev([] { (void)rt_warmup(RT_WARM_DEVICE); });
+    Joiner join_dev{warm_dev};
     if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";
     const auto t0 = std::chrono::steady_clock::now();
@@ -109,6 +122,8 @@ int main(int argc, char** argv) {
         return 4;
     }
     const auto t2 = std::chrono::steady_clock::now();
+    if (warm_host.joinable()) warm_host.join();
+    if (warm_dev.joinable()) warm_dev.join();
     teardown.done = true;
     // With one GPU the library holds no communicators: its device memory is
     // the process's and goes with it at the _Exit below.  Several GPUs:

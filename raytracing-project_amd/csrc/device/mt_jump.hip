@@ -19,6 +19,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <mutex>
 #include <string>
 #include <stdint.h>
@@ -537,28 +538,36 @@ static void locate_poly_file() {
     });
 }
 
-hipError_t JitterPlan::build(int K_blocks, int levels_needed, hipStream_t stream) {
-    release();
+// The tree's tap lists (host only, cached per process): level-major, so a
+// plan of fewer levels uses a prefix.  rt_warmup(RT_WARM_HOST) computes them
+// on a helper thread while the process initialises HIP.
+namespace {
+struct HostTaps {
+    int K = 0, levels = 0;
+    std::vector<uint16_t> taps;
+    std::vector<int32_t> off;
+};
+std::mutex g_taps_mu;
+std::shared_ptr<const HostTaps> g_taps;
+}  // namespace
+
+std::shared_ptr<const HostTaps> host_taps(int K_blocks, int levels_needed) {
+    std::lock_guard<std::mutex> lk(g_taps_mu);
+    if (g_taps && g_taps->K == K_blocks && g_taps->levels >= levels_needed) return g_taps;
     locate_poly_file();
     std::vector<uint32_t> polys = mt_tree_polys(K_blocks, levels_needed);
     // the set coefficients of every polynomial, in order (~2.3 M taps for 4
     // levels): sized by popcount, then one ctz walk per word (a bit-by-bit
-    // scan took ~40 ms of the CLI's one-time setup), written straight into
-    // the page-locked staging: [seed window | taps]
+    // scan took ~40 ms of the CLI's one-time setup)
+    auto T = std::make_shared<HostTaps>();
+    T->K = K_blocks;
+    T->levels = levels_needed;
     const size_t n_poly = (size_t)levels_needed * (kMTRadix - 1);
     size_t n_taps = 0;
     for (size_t k = 0; k < n_poly * kPolyWords32; ++k) n_taps += (size_t)__builtin_popcount(polys[k]);
-    const size_t win_bytes = (size_t)N * sizeof(uint32_t);
-    const size_t taps_cap = n_taps + 8;
-    hipError_t e = hipHostMalloc(&h_stage, win_bytes + taps_cap * sizeof(uint16_t), hipHostMallocDefault);
-    if (e != hipSuccess) {
-        h_stage = nullptr;
-        return e;
-    }
-    uint32_t* win = static_cast<uint32_t*>(h_stage);
-    uint16_t* taps = reinterpret_cast<uint16_t*>(static_cast<char*>(h_stage) + win_bytes);
+    T->taps.resize(n_taps);
     size_t o = 0;
-    off.assign(1, 0);
+    T->off.assign(1, 0);
     for (int j = 0; j < levels_needed; ++j)
         for (int m = 0; m < kMTRadix; ++m) {
             if (m > 0) {
@@ -566,11 +575,38 @@ hipError_t JitterPlan::build(int K_blocks, int levels_needed, hipStream_t stream
                 for (int w = 0; w < kPolyWords32; ++w)
                     for (uint32_t b = P[w]; b; b &= b - 1) {
                         const int i = w * 32 + __builtin_ctz(b);
-                        if (i < kMTDeg) taps[o++] = (uint16_t)i;
+                        if (i < kMTDeg) T->taps[o++] = (uint16_t)i;
                     }
             }
-            off.push_back((int32_t)o);
+            T->off.push_back((int32_t)o);
         }
+    T->taps.resize(o);
+    g_taps = T;
+    return T;
+}
+
+void mt_prefetch_host_taps() {
+    locate_poly_file();
+    const int levels = std::min(MAX_LEVELS, mt_poly_file_levels(kTableK));
+    if (levels > 0) (void)host_taps(kTableK, levels);   // (never the slow computed path here)
+}
+
+hipError_t JitterPlan::build(int K_blocks, int levels_needed, hipStream_t stream) {
+    release();
+    const std::shared_ptr<const HostTaps> T = host_taps(K_blocks, levels_needed);
+    // page-locked staging: [seed window | taps of the first levels_needed levels]
+    const size_t win_bytes = (size_t)N * sizeof(uint32_t);
+    const size_t o = (size_t)T->off[(size_t)levels_needed * kMTRadix];
+    const size_t taps_cap = o + 8;
+    hipError_t e = hipHostMalloc(&h_stage, win_bytes + taps_cap * sizeof(uint16_t), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        h_stage = nullptr;
+        return e;
+    }
+    uint32_t* win = static_cast<uint32_t*>(h_stage);
+    uint16_t* taps = reinterpret_cast<uint16_t*>(static_cast<char*>(h_stage) + win_bytes);
+    std::memcpy(taps, T->taps.data(), o * sizeof(uint16_t));
+    off.assign(T->off.begin(), T->off.begin() + (size_t)levels_needed * kMTRadix + 1);
     for (int k = 0; k < 8; ++k) taps[o + k] = 0;
     const size_t n_up = o + 8;
     mt_first_window(12345u, win);

@@ -107,6 +107,10 @@ struct JitterTable {
     hipError_t ensure(int64_t n_need, hipStream_t stream);   // synchronous when it grows
     void release();
 };
+// Host-only: the checkpoint tree's tap lists for every level the shipped
+// polynomial file holds, cached for the process (rt_warmup RT_WARM_HOST runs
+// it on a helper thread while the caller initialises HIP).
+void mt_prefetch_host_taps();
 // Scratch for mt_launch_fill's segment/range lists.
 size_t mt_fill_scratch_bytes(const std::vector<JRange>& ranges);
 // Regenerate the draws of `ranges` from the table (table.ensure must cover them).

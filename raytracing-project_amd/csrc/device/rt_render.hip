@@ -1018,6 +1018,33 @@ hipError_t rtamd::host_copy_async(void* dst, const void* src, size_t n, hipStrea
     return hipGetLastError();
 }
 
+extern "C" int rt_warmup(int what) {
+    if (what & ~(RT_WARM_HOST | RT_WARM_DEVICE)) {
+        rtamd::set_last_error("rt_warmup: unknown bits");
+        return RT_ERR_INVALID_ARG;
+    }
+    if (what & RT_WARM_HOST) {
+        try {
+            rtamd::mt_prefetch_host_taps();
+        } catch (const std::exception& e) {
+            rtamd::set_last_error(std::string("rt_warmup: ") + e.what());
+            return RT_ERR_PROCESSING;
+        }
+    }
+    if (what & RT_WARM_DEVICE) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+            rtamd::set_last_error("rt_warmup: no HIP device available");
+            return RT_ERR_NO_DEVICE;
+        }
+        // the FP64 render kernels' code object (one per fat binary and
+        // device, loaded at its first use; hipFuncGetAttributes loads it)
+        hipFuncAttributes a{};
+        HIP_TRY(hipFuncGetAttributes(&a, rtd::std_kernel(false, false, false, true, false)));
+    }
+    return RT_OK;
+}
+
 hipError_t rtamd::warm_copy_engine(hipStream_t st) {
     static std::mutex mu;
     static bool done = false;

@@ -317,6 +317,24 @@ bool mt_load_tree_polys(const std::string& path, int K_blocks, int levels, std::
     return true;
 }
 
+int mt_poly_file_levels(int K_blocks) {
+    std::string file;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        file = g_poly_file;
+    }
+    if (file.empty()) return 0;
+    FILE* f = std::fopen(file.c_str(), "rb");
+    if (!f) return 0;
+    char magic[8];
+    uint32_t hdr[4];
+    const bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "MTJPOLY1", 8) == 0 &&
+                    std::fread(hdr, 4, 4, f) == 4 && (int)hdr[0] == K_blocks && hdr[1] <= 16 &&
+                    hdr[2] == (uint32_t)kPolyWords32;
+    std::fclose(f);
+    return ok ? (int)hdr[1] : 0;
+}
+
 bool mt_save_tree_polys(const std::string& path, int K_blocks, int levels) {
     const std::vector<uint32_t> p = mt_tree_polys_computed(K_blocks, levels);
     FILE* f = std::fopen(path.c_str(), "wb");

@@ -53,6 +53,8 @@ std::vector<uint32_t> mt_tree_polys(int K_blocks, int levels);
 // A missing, short or corrupt file is ignored (the polynomials are computed).
 void mt_set_poly_file(const std::string& path);
 bool mt_save_tree_polys(const std::string& path, int K_blocks, int levels);
+// Levels the configured poly file holds for K (0: none / unusable header).
+int mt_poly_file_levels(int K_blocks);
 // Reads the first `levels` levels from `path` into out; false if unusable.
 bool mt_load_tree_polys(const std::string& path, int K_blocks, int levels, std::vector<uint32_t>& out);
 // mt_tree_polys computed in this process, ignoring the file (tests).
