@@ -441,20 +441,25 @@ __device__ __forceinline__ real clamp1(real x) {   // geometry.cpp:152-156
     return x;
 }
 
-// Pokeball::pick_region_material (geometry.cpp:163-180)
+// Pokeball::pick_region_material (geometry.cpp:163-180) given its local unit
+// position u = (p - c) / r (the same three divisions as Sphere's outward
+// normal at p, geometry.cpp:31: callers that have that normal pass it)
 template <class CT>
-__device__ __forceinline__ int pick_region(const NodeT* nd, V3 p, CT& cnt) {
+__device__ __forceinline__ int pick_region_u(const NodeT* nd, V3 u, CT& cnt) {
     cnt.inc(RT_OPC_POKE_REGION);
     const real* v = nd->v;
-    const real r = v[3];
-    const auto uq = div3(p.x - v[0], p.y - v[1], p.z - v[2], r);
-    V3 u = v3(uq.x, uq.y, uq.z);
     // ang = acos(x) <= btnOuter / ang >= inner as x >= xb / x <= xi: the
     // thresholds of the host's (the reference's) acos, rtamd::pokeball_thresholds
     const real x = clamp1(dot3(u, v3(v[7], v[8], v[9])));
     if (x >= v[rtamd::kPokeXb]) return (x <= v[rtamd::kPokeXi]) ? nd->mats[RT_PB_RING] : nd->mats[RT_PB_BUTTON];
     if (fabs_r(u.y) <= v[4]) return nd->mats[RT_PB_BELT];
     return (u.y >= RV(0.0)) ? nd->mats[RT_PB_TOP] : nd->mats[RT_PB_BOTTOM];
+}
+template <class CT>
+__device__ __forceinline__ int pick_region(const NodeT* nd, V3 p, CT& cnt) {
+    const real* v = nd->v;
+    const auto uq = div3(p.x - v[0], p.y - v[1], p.z - v[2], v[3]);
+    return pick_region_u(nd, v3(uq.x, uq.y, uq.z), cnt);
 }
 
 // Leaf Primitive::intersect for the three leaf kinds.
@@ -1287,7 +1292,7 @@ __device__ __forceinline__ void leaf_shading(const NodeT* nd, const DRay& r, V3 
     const auto oq = div3(p.x - nd->v[0], p.y - nd->v[1], p.z - nd->v[2], rad);
     const V3 outward = v3(oq.x, oq.y, oq.z);
     set_face_normal(h, r, outward);
-    h.mat = nd->kind == RT_NODE_SPHERE ? nd->mat : pick_region(nd, p, cnt);
+    h.mat = nd->kind == RT_NODE_SPHERE ? nd->mat : pick_region_u(nd, outward, cnt);   // (u = the outward normal)
 }
 
 // Resolve a compact hit reference on frame ray r into (n, ff, mat).
@@ -1448,11 +1453,33 @@ __device__ bool scene_intersect(const DevScene& S, const DRay& r, real tmin, rea
     return true;
 }
 
+// A lane's segment [o + t0 d, o + t1 d] against a bare half-space's plane
+// (cull record type 3: c0 = (n, n.p), c1.y = its magnitude): false only if
+// both ends lie on the same side by more than the f32 margin, where the
+// plane crossing t of HalfSpace::intersect (geometry.cpp:90-106) is outside
+// [t0, t1] in every rounding.  NaN passes.
+__device__ __forceinline__ bool plane_touch(const float4 c0, const float4 c1, const FRay& r, float t0, float t1) {
+    const float ax = __builtin_fmaf(t0, r.dx, r.ox), ay = __builtin_fmaf(t0, r.dy, r.oy), az = __builtin_fmaf(t0, r.dz, r.oz);
+    const float bx = __builtin_fmaf(t1, r.dx, r.ox), by = __builtin_fmaf(t1, r.dy, r.oy), bz = __builtin_fmaf(t1, r.dz, r.oz);
+    const float sa = __builtin_fmaf(c0.x, ax, __builtin_fmaf(c0.y, ay, c0.z * az)) - c0.w;
+    const float sb = __builtin_fmaf(c0.x, bx, __builtin_fmaf(c0.y, by, c0.z * bz)) - c0.w;
+    const float mag = __builtin_fabsf(ax) + __builtin_fabsf(ay) + __builtin_fabsf(az) + __builtin_fabsf(bx) +
+                      __builtin_fabsf(by) + __builtin_fabsf(bz) + c1.y + 1.0f;
+    const float m = 1e-5f * mag;
+    return !((sa > m) & (sb > m)) & !((sa < -m) & (sb < -m));
+}
+
 // Scene::occluded (scene.cpp:33-42): any hit; per-lane early exit.
+// lazy: r.d is the shadow direction BEFORE the Ray constructor's
+// re-normalisation (core.h:278); the f32 culls use it as it is (a few FP64
+// ulps from the normalised one, far inside their margins) and the exact ray
+// is formed only once an object survives them (as scene_occluded_capsule).
 template <bool EAGER, bool DEEP, class CT>
-__device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real tmax, CT& cnt) {
+__device__ bool scene_occluded(const DevScene& S, const DRay& r0, real tmin, real tmax, CT& cnt, bool lazy = false) {
     bool hit = false;
-    const FRay fr = to_fray(r);
+    DRay r = r0;
+    bool r_exact = !lazy;
+    const FRay fr = to_fray(r0);
     const float ftmin = (float)tmin, ftmax = (float)tmax;
     for (int o = 0; o < S.n_objs; ++o) {
         if (__all(hit)) break;
@@ -1464,8 +1491,19 @@ __device__ bool scene_occluded(const DevScene& S, const DRay& r, real tmin, real
                 if (ob.kind == rtamd::OBJ_GROUP) o += ob.m;
                 continue;
             }
+        } else if (S.cull && ob.kind != rtamd::OBJ_GROUP) {
+            // a bare half-space: skipped unless some lane's segment crosses its plane
+            const float4 c1 = S.ctab[2 * o + 1];
+            if (__float_as_int(c1.x) == 3 && !__any(!hit && plane_touch(S.ctab[2 * o], c1, fr, ftmin, ftmax))) {
+                cnt.inc(RT_OPC_CULLED);
+                continue;
+            }
         }
         if (ob.kind == rtamd::OBJ_GROUP) continue;
+        if (!r_exact) {   // Ray::Ray (core.h:278) of the shadow ray (shading.cpp:98)
+            r.d = normalized(r.d);
+            r_exact = true;
+        }
         // every lane evaluates (no divergent region between the loop's
         // wave-wide tests, see scene_occluded_wave); op-counting builds take
         // the same path and count only the reference's calls (lanes without
@@ -2613,9 +2651,9 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 cnt.pb(PH_SHADOW);
                 occ = scene_occluded_capsule<EAGER, DEEP, UO, false>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
                 cnt.pe(PH_SHADOW);
-            } else {
-                const DRay sr = make_ray(so, wi);
-                if (need) occ = scene_occluded<EAGER, DEEP>(S, sr, eps, max_t, cnt);
+            } else if (need) {
+                // (the direction's re-normalisation happens inside, when needed)
+                occ = scene_occluded<EAGER, DEEP>(S, DRay{so, wi}, eps, max_t, cnt, true);
             }
             if (need) {
                 ++n_occl;
