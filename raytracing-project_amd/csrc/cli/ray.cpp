@@ -101,7 +101,10 @@ int main(int argc, char** argv) {
     const auto t_hip1 = std::chrono::steady_clock::now();
     // the render kernels' code object (~5 ms) loads on a helper thread while
     // this one compiles and uploads the scene and builds the jitter table
-    std::thread warm_dev([] { (void)rt_warmup(RT_WARM_DEVICE); });
+    // (RAY_WARM_DEVICE=0: not at all, for measurement)
+    const char* wd = std::getenv("RAY_WARM_DEVICE");
+    std::thread warm_dev;
+    if (!(wd && *wd == '0')) warm_dev = std::thread([] { (void)rt_warmup(RT_WARM_DEVICE); });
     Joiner join_dev{warm_dev};
     if (paper_mode) std::cout << "Rendering in paper mode (" << W << "x" << H << ")\n";
     else std::cout << "Rendering with 8 spp (" << W << "x" << H << ")\n";

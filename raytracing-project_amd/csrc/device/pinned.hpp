@@ -70,10 +70,10 @@ struct PinnedArena {
 // r06d_first_op.txt: pageable or page-locked alike; a kernel's own first
 // launch ~0.3 ms), so a frame's uploads never use the copy engines.
 hipError_t host_copy_async(void* dst, const void* src_pinned, size_t n, hipStream_t st);
-// Once per process: a 16-byte device-to-host copy-engine transfer on st, so
-// that the runtime's one-time copy-engine setup (host time in the call)
-// runs while the frame's kernels execute instead of in front of the
-// frame's read-back.
+// Once per process: a 1 MiB device-to-host read-back into pageable memory on
+// st, so that the runtime's one-time set-up of that path (~8 ms of host time
+// in the call, profiles/r06d_first_op.txt) runs while the frame's first trace
+// executes instead of in front of the frame's read-back.
 hipError_t warm_copy_engine(hipStream_t st);
 
 // H2D through the arena: page-locked staging + k_host_copy (pageable

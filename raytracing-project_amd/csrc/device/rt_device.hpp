@@ -1792,7 +1792,28 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
             if (cap && ob.npb > 0 && exec_full()) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
                 const bool in = lane < ob.npb;
-                if (!__any(in && capsule_touch(g, K))) {
+                const uint64_t cb = __ballot(in && capsule_touch(g, K));   // leaves the capsule reaches
+                bool seg = cb != 0;
+#ifndef RT_NO_LANE_LEAF_TEST
+                // Then each lane's own segment against those leaf balls: the
+                // object can occlude a lane only at a point within the slop
+                // of one of its leaves' balls (leaf_prefilter,
+                // scene_compile.cpp), so unless some lane's segment touches
+                // one of them, no lane's query can hit it.  (A shadow ray
+                // leaving the object's own surface starts outside every leaf
+                // ball by its eps offset, so the self-shadow queries of a
+                // wave on the object - whose capsule always reaches the
+                // leaves around it - skip the evaluation.)  The exec mask is
+                // full here (checked above), so cb is the whole wave's.
+                if (seg) {
+                    seg = false;
+                    for (uint64_t mm = cb; mm && !seg; mm &= mm - 1) {
+                        const float* gk = S.gb + 4 * (ob.pb0 + __builtin_ctzll(mm));
+                        seg = __any(need && !hit && ball_touch(gk, fr, ftmin, ftmax));
+                    }
+                }
+#endif
+                if (!seg) {
                     if (need) cnt.inc(RT_OPC_CULLED);
                     cnt.pe(PH_OBJ_PREF);
                     continue;

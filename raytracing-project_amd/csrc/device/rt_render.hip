@@ -1049,13 +1049,19 @@ hipError_t rtamd::warm_copy_engine(hipStream_t st) {
     static std::mutex mu;
     static bool done = false;
     static void* dev = nullptr;
-    static void* host = nullptr;
+    static std::vector<char> host;
     std::lock_guard<std::mutex> lk(mu);
     if (done) return hipSuccess;
     done = true;   // (one attempt: the copy is an optimisation only)
+    // a 1 MiB read-back into pageable memory takes the same runtime path as
+    // a frame's read-back (its staging set-up is the ~8 ms first-copy cost);
+    // issued behind the first trace launch, the host spends that time while
+    // the trace runs (the call returns when the copy has run)
+    constexpr size_t kBytes = (size_t)1 << 20;
     rtamd::SetupTimer tm(rtamd::kSetupCopyEngine);
-    if (hipMalloc(&dev, 16) != hipSuccess || hipHostMalloc(&host, 16, hipHostMallocDefault) != hipSuccess) return hipSuccess;
-    return hipMemcpyAsync(host, dev, 16, hipMemcpyDeviceToHost, st);
+    if (hipMalloc(&dev, kBytes) != hipSuccess) return hipSuccess;
+    host.resize(kBytes);
+    return hipMemcpyAsync(host.data(), dev, kBytes, hipMemcpyDeviceToHost, st);
 }
 
 int rtamd::wave_cull_min() {
