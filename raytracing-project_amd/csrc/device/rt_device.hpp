@@ -309,6 +309,7 @@ struct DevScene {
     int n_lights, n_objs;
     int n_dlights;
     int n_bounded;   // objects with a bounding ball (wave-level culling pays only when > 0)
+    int n_lead;      // CompiledScene::n_lead: unbounded objects ahead of every bounded one (0 in the BVH kernels)
     int cam_nx, cam_ny;
     int rec_limit, cull;
     real eye[3], P[3], Lx, Ly;
@@ -1734,9 +1735,29 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
     bool lb_ready = false;
     Cone LB{f2(0.0f, 0.0f), f2(0.0f, 0.0f), 0.0f, 0.0f, -1.0f, 1.0f, 0.0f, 0.0f};
     bool hit = false;
-    const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
+    // the lead objects (CompiledScene::n_lead: unbounded, ahead of every
+    // bounded one) as pseudo-chunk -1, each tested on its own - a bare
+    // half-space by every querying lane's segment against its plane - then
+    // the transposed tests over the objects behind them
+    const int lead = BV ? 0 : S.n_lead;
+    const int nch = BV ? S.n_chunks : (S.n_objs - lead + 63) >> 6;
     uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 some querying segment can reach
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int ch = lead > 0 ? -1 : 0; ch < nch; ++ch) {
+        int base;
+        uint64_t m;
+        if (ch < 0) {
+            base = 0;
+            m = 0;
+            for (int o = 0; o < lead; ++o) {
+                const float4 c1 = S.ctab[2 * o + 1];
+                const int type = __float_as_int(c1.x);
+                const bool pass = type == 1 || (type == 3 && (!(cap && S.cull) ||
+                                                               __any(need && plane_touch(S.ctab[2 * o], c1, fr, ftmin, ftmax))));
+                if (pass) m |= 1ull << o;
+                else if (type != 0 && need) cnt.inc(RT_OPC_CULLED);
+            }
+            cnt.pe(PH_WAVE_SETUP);
+        } else {
         if constexpr (BV) {
             if ((ch & 63) == 0) {
                 const int c = ch + lane;
@@ -1751,7 +1772,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
                 continue;
             }
         }
-        const int base = ch << 6;
+        base = lead + (ch << 6);
         const int nc = S.n_objs - base;
         const int j = base + lane;
         // the object's cull record (CompiledScene::ctab): one 32-byte load on
@@ -1763,7 +1784,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
                                : __float_as_int(c1.x) != 0);
         // (lane j tests object j only with the whole wave active; otherwise
         // every object of the chunk is a candidate)
-        uint64_t m = (cap && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        m = (cap && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
 #if defined(RT_ABL) && RT_ABL == 2   // diagnostic: setup + transposed test only
         if (m != 12345) return false;
@@ -1777,6 +1798,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
                 }
                 cnt_add(cnt, RT_OPC_CULLED, skipped);
             }
+        }
         }
         while (m) {
             const int o = base + __builtin_ctzll(m);
@@ -2390,9 +2412,22 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     real wts = RV(0.0);
     int wcode = 0;
     const float ftmin = (float)tmin;
-    const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
+    // the lead objects (CompiledScene::n_lead: unbounded, ahead of every
+    // bounded one) first, in order, as pseudo-chunk -1; then the transposed
+    // tests over the objects behind them (the reference's order throughout)
+    const int lead = BV ? 0 : S.n_lead;
+    const int nch = BV ? S.n_chunks : (S.n_objs - lead + 63) >> 6;
     uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 the bundle can reach
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int ch = lead > 0 ? -1 : 0; ch < nch; ++ch) {
+        int base;
+        uint64_t m;
+        if (ch < 0) {
+            base = 0;
+            m = 0;
+            for (int o = 0; o < lead; ++o)
+                if (__float_as_int(S.ctab[2 * o + 1].x) != 0) m |= 1ull << o;
+            cnt.pe(PH_WAVE_SETUP);
+        } else {
         if constexpr (BV) {
             if ((ch & 63) == 0) {
                 const int c = ch + lane;
@@ -2408,7 +2443,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 continue;
             }
         }
-        const int base = ch << 6;
+        base = lead + (ch << 6);
         const int j = base + lane;
         const int jr = j < S.n_objs ? j : S.n_objs - 1;   // (see scene_occluded_wave)
         const float4 c0 = S.ctab[2 * jr], c1 = S.ctab[2 * jr + 1];
@@ -2416,7 +2451,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
         const bool pass = (j < S.n_objs) & (type != 0) &
                           ((type != 2) | wide | cone_touch(c0, c1.y, K));
         const int nc = S.n_objs - base;
-        uint64_t m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
+        m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
         if constexpr (!std::is_same<CT, Cnt<false>>::value) {
             int skipped = 0;
@@ -2425,6 +2460,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 if (k != rtamd::OBJ_GROUP && k != rtamd::OBJ_NEVER && !((m >> (o - base)) & 1)) ++skipped;
             }
             if (valid) cnt_add(cnt, RT_OPC_CULLED, skipped);
+        }
         }
         while (m) {
             const int o = base + __builtin_ctzll(m);

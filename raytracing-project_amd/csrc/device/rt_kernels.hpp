@@ -507,6 +507,7 @@ DevScene make_scene(const SceneView& V, bool bv = false) {
     S.n_lights = V.n_lights;
     S.n_dlights = V.n_dlights;
     S.n_bounded = V.n_bounded;
+    S.n_lead = bv ? 0 : V.n_lead;
     S.n_objs = bv ? V.n_wobjs : V.n_objs;
     S.cam_nx = V.cam_nx;
     S.cam_ny = V.cam_ny;

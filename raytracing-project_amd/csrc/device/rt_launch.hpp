@@ -84,6 +84,7 @@ struct SceneView {
     int n_lights, n_dlights, n_objs;
     int n_bounded;
     int wave_cull;   // wave-level culls: cull && n_bounded >= wave_cull_min() (host-decided)
+    int n_lead;      // CompiledScene::n_lead (0: none / RT_LEAD=0)
     int cam_nx, cam_ny;
     int rec_limit, cull;
     double eye[3], P[3], Lx, Ly;

@@ -578,6 +578,10 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     S.rec_limit = d.recursion_limit;
     S.cull = (flags & RT_FLAG_NO_CULL) ? 0 : 1;
     S.wave_cull = S.cull && S.n_bounded >= rtamd::wave_cull_min();
+    {
+        static const bool lead_on = [] { const char* e = std::getenv("RT_LEAD"); return !(e && *e == '0'); }();
+        S.n_lead = lead_on ? cs.n_lead : 0;   // (RT_LEAD=0: measurement A/B)
+    }
     for (int i = 0; i < 3; ++i) {
         S.eye[i] = d.camera.eye[i];
         S.P[i] = d.camera.P[i];

@@ -503,6 +503,18 @@ public:
             }
             std::memcpy(&c[4], &type, sizeof(int));
         }
+        {
+            auto type_of = [&](size_t j) {
+                int t;
+                std::memcpy(&t, &cs.ctab[8 * j + 4], sizeof t);
+                return t;
+            };
+            size_t lead = 0;
+            while (lead < cs.objs.size() && (type_of(lead) == 1 || type_of(lead) == 3)) ++lead;
+            bool ok = lead <= 64;
+            for (size_t j = lead; ok && j < cs.objs.size(); ++j) ok = type_of(j) != 1 && type_of(j) != 3;
+            cs.n_lead = ok ? (int)lead : 0;
+        }
         build_wave_bvh(cs);
         light_records(cs.ctab.data(), cs.objs.size(), 8, d_.lights, d_.n_lights, cs.lrec);
         light_records(cs.wctab.data(), cs.wobjs.size(), 8, d_.lights, d_.n_lights, cs.lwrec);

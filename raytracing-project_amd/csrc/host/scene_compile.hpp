@@ -114,6 +114,13 @@ struct CompiledScene {
     int max_ray_depth = 0;   // transform nesting on any path of an eager program (chains need no stack)
     int max_ivl_depth = 0;   // interval stack depth on any path
     bool has_eager = false;  // some object needs the eager interpreter
+    // Unbounded objects (ctab type 1 / 3) that precede every bounded one in
+    // objs order (0 if an unbounded object follows a bounded one, or more
+    // than 64 lead).  The wave kernels without the BVH test these one by one
+    // before the transposed tests, which then cover only the objects behind
+    // them: a floor plus 64 spheres (config 5) is one 64-object chunk, not
+    // two.  Visiting them first keeps the reference's order (closest-hit ties).
+    int n_lead = 0;
     bool has_pokeball = false;
 };
 

@@ -1,0 +1,11 @@
+# Parity subset on the in-tree build, then RT_LEAD=0 / 1 A/B on configs ${CFGS:-5 6 4}.
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullres_parity.py tests/test_gpu_crowd.py tests/test_gpu_bvh.py tests/test_gpu_recursion.py tests/test_gpu_edges.py tests/test_gpu_deep.py tests/test_gpu_dist_threads.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r06k_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r06k_tests.log; exit 1; }
+tail -1 gpurun_out/r06k_tests.log
+for c in ${CFGS:-5 6 4}; do
+for i in 1 2; do
+for v in 0 1; do
+  RT_LEAD=$v timeout -k 10 200 python bench.py --config $c --no-cpu --no-pmc --no-cli --fp32-steps 0 --steps ${STEPS:-100} --warmup 3 > gpurun_out/ab_${c}_lead$v_$i.json 2> gpurun_out/ab_${c}_lead$v_$i.err || { echo "bench $c $v failed"; tail gpurun_out/ab_${c}_lead$v_$i.err; exit 1; }
+  tail -1 gpurun_out/ab_${c}_lead$v_$i.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('cfg $c lead=$v', 'frame_ms', d['ms_per_step'], 'kernel_ms', d['roofline']['kernel_ms'], 'value', d['value'])"
+done; done; done
