@@ -1686,7 +1686,7 @@ __device__ __forceinline__ bool record_touch(const float4 c0, const float4 c1, c
 // transposed test per 64 chunks skips every chunk no querying segment can
 // reach, then each surviving chunk runs the object test below.  Occlusion is
 // an OR over objects, so the order is free.
-template <bool EAGER, bool DEEP, bool UO, bool BV = false, class CT>
+template <bool EAGER, bool DEEP, bool UO, bool BV = false, bool LEAD = false, class CT>
 __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real tmin, real tmax, bool need, bool wave_ok,
                                     CT& cnt) {
 #if defined(RT_ABL) && RT_ABL == 1   // diagnostic ablation builds only (wrong images): no shadow queries
@@ -1739,7 +1739,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
     // bounded one) as pseudo-chunk -1, each tested on its own - a bare
     // half-space by every querying lane's segment against its plane - then
     // the transposed tests over the objects behind them
-    const int lead = BV ? 0 : S.n_lead;
+    const int lead = (BV || !LEAD) ? 0 : S.n_lead;
     const int nch = BV ? S.n_chunks : (S.n_objs - lead + 63) >> 6;
     uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 some querying segment can reach
     for (int ch = lead > 0 ? -1 : 0; ch < nch; ++ch) {
@@ -2374,7 +2374,7 @@ __device__ __forceinline__ bool cone_touch(const float* g, const Cone& K) {
 // loop would: of two objects hitting at the same t, the later (in the
 // reference's order) wins if it accepts t == tmax (spheres, half-spaces,
 // pokeballs: rtamd::accepts_tie), else the earlier one.
-template <bool EAGER, bool DEEP, bool BV = false, class CT>
+template <bool EAGER, bool DEEP, bool BV = false, bool LEAD = false, class CT>
 __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin, real tmax, real& t_best,
                                      DHit& best, bool wave_ok, CT& cnt, bool valid = true) {
     cnt.pb(PH_WAVE_SETUP);
@@ -2415,7 +2415,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
     // the lead objects (CompiledScene::n_lead: unbounded, ahead of every
     // bounded one) first, in order, as pseudo-chunk -1; then the transposed
     // tests over the objects behind them (the reference's order throughout)
-    const int lead = BV ? 0 : S.n_lead;
+    const int lead = (BV || !LEAD) ? 0 : S.n_lead;
     const int nch = BV ? S.n_chunks : (S.n_objs - lead + 63) >> 6;
     uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 the bundle can reach
     for (int ch = lead > 0 ? -1 : 0; ch < nch; ++ch) {
@@ -2611,7 +2611,10 @@ __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
 #ifndef RT_STD_UO
 #define RT_STD_UO false
 #endif
-template <bool EAGER, bool DEEP, bool DL, int WV, bool UO = RT_STD_UO, class CT>
+// LEAD: the wave queries handle CompiledScene::n_lead (the paper and
+// recursion kernels; in the lean standard kernel the extra path cost
+// registers: config 4 kernel 7.2 -> 7.6 ms, profiles/r06_ab/ab_lead.txt)
+template <bool EAGER, bool DEEP, bool DL, int WV, bool UO = RT_STD_UO, bool LEAD = false, class CT>
 __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t& n_occl, CT& cnt,
                     bool valid = true) {
     // valid = false: a lane of the wave that has nothing to shade (a primary
@@ -2706,7 +2709,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
                 cnt.pe(PH_SHADOW);
             } else if constexpr (WV) {
                 cnt.pb(PH_SHADOW);
-                occ = scene_occluded_capsule<EAGER, DEEP, UO, false>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
+                occ = scene_occluded_capsule<EAGER, DEEP, UO, false, LEAD>(S, DRay{so, wi}, eps, max_t, need, wave_full, cnt);
                 cnt.pe(PH_SHADOW);
             } else if (need) {
                 // (the direction's re-normalisation happens inside, when needed)
@@ -2854,7 +2857,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         h.ff = 1;
         if (eval) ++n_isect;
         cnt.pb(PH_PRIMARY);
-        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2)>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
+        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2), true>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
         cnt.pe(PH_PRIMARY);
         const bool sh = eval && hit;
         // ---- the step's children, pushed before shading (tracer.cpp:38-68)
@@ -2904,7 +2907,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         }
         const V3 wo = normalized(vneg(r.d));
         V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
-        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV>(S, ht, h, wo, n_occl, cnt, sh);
+        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV, RT_STD_UO, true>(S, ht, h, wo, n_occl, cnt, sh);
         // the step's value (a finished lane's colour is in memory, so nothing
         // but the stack state is carried across steps)
         V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));
