@@ -98,7 +98,10 @@ int mt_levels_needed(int K, int64_t q1);
 // (8-rank share of config 4: 0.174 -> 0.086 ms) at 4x the table (66 MB for
 // a 4K frame, built once per device).  bin/mt_polygen writes the tree
 // polynomials for this K (tests/test_mt_poly_file.py keeps the two in step).
-constexpr int kTableK = 16;
+#ifndef RT_TABLE_K
+#define RT_TABLE_K 16
+#endif
+constexpr int kTableK = RT_TABLE_K;   // (RT_TABLE_K: measurement A/B; lib/mt19937_tree.polys must be written for it)
 struct JitterTable {
     JitterPlan plan;                  // K = kTableK
     uint32_t* d_table = nullptr;      // [cap][624] windows

@@ -48,6 +48,11 @@
 namespace {
 
 constexpr int kChunks = 4;
+// Paper frames gather one code byte per pixel, so their chunks hide little
+// transfer, while every chunk adds a launch tail of the costly paper waves:
+// 2 chunks project config 5 at 8 ranks 5.21-5.23x -> 5.46-5.56x, at 4 ranks
+// 3.04 -> 3.12-3.18x (1: 4.58x, 3: 5.30x; profiles/r06_ab/ab_dist_chunks.txt).
+constexpr int kPaperChunks = 2;
 constexpr int kSplitSlots = 10;   // rt_dist_frame_split (include/rt.h)   // pipeline units per rank (chunk k gathered while k+1 is traced)
 
 #define HIP_TRY(expr)                                                                            \
@@ -628,13 +633,13 @@ __global__ void k_test_stall(unsigned long long max_ticks) {
 
 enum { kInjectTraceFail = 1, kInjectStall = 2, kInjectSetupFail = 3 };
 
-// Row chunks per rank and frame (each one gather): kChunks, or
+// Row chunks per rank and frame (each one gather): kChunks (paper: kPaperChunks), or
 // RT_DIST_CHUNKS (standard mode) / RT_DIST_CHUNKS_PAPER from the environment
 // (measurement A/B; 1 .. kChunks).
 int frame_chunks(int mode) {
     static const int c[2] = {
         [] { const char* e = std::getenv("RT_DIST_CHUNKS"); return e && *e ? std::atoi(e) : kChunks; }(),
-        [] { const char* e = std::getenv("RT_DIST_CHUNKS_PAPER"); return e && *e ? std::atoi(e) : kChunks; }()};
+        [] { const char* e = std::getenv("RT_DIST_CHUNKS_PAPER"); return e && *e ? std::atoi(e) : kPaperChunks; }()};
     return std::min(kChunks, std::max(1, c[mode == RT_MODE_PAPER ? 1 : 0]));
 }
 

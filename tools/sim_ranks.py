@@ -171,7 +171,7 @@ def product_ranks(args):
             base = worst
         m = max(len(rtamd.dist_rows(H, N, r, mode)) for r in range(N))   # rows per rank slot (dist_frame's m)
         strip = frame_dist.strip_for(mode)
-        nch = int(os.environ.get("RT_DIST_CHUNKS_PAPER" if mode == 1 else "RT_DIST_CHUNKS", "4"))
+        nch = int(os.environ.get("RT_DIST_CHUNKS_PAPER", "2") if mode == 1 else os.environ.get("RT_DIST_CHUNKS", "4"))
         a_last, b_last = frame_dist.chunk_bounds(m, max(1, min(4, nch)), strip)[-1]
         bpp = 1 if mode == 1 else (3 if args.rgb8 else 24)   # paper: one code byte per pixel
         last_chunk = (b_last - a_last) * W * bpp
