@@ -2241,7 +2241,22 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
                 const int k = ob.pb0 + (lane < ob.npb ? lane : 0);
                 const float4 g0 = lgb[2 * k], g1 = lgb[2 * k + 1];
                 const bool in = lane < ob.npb;
-                if (!__any(in && lrec_ball_cone(g0, g1.y, g1.z, K))) {
+                const uint64_t cbm = __ballot(in && lrec_ball_cone(g0, g1.y, g1.z, K));
+                bool seg = cbm != 0;
+#ifndef RT_NO_LANE_LEAF_TEST
+                // each lane's own segment against the leaf balls the cone
+                // reaches (see scene_occluded_capsule): no touch, no hit
+                if (seg) {
+                    const FRay sfr = to_fray(r0);
+                    const float st0 = (float)tmin, st1 = (float)tmax;
+                    seg = false;
+                    for (uint64_t mm = cbm; mm && !seg; mm &= mm - 1) {
+                        const float* gk = S.gb + 4 * (ob.pb0 + __builtin_ctzll(mm));
+                        seg = __any(need && !hit && ball_touch(gk, sfr, st0, st1));
+                    }
+                }
+#endif
+                if (!seg) {
                     if (need) cnt.inc(RT_OPC_CULLED);
                     cnt.pe(PH_OBJ_PREF);
                     continue;
