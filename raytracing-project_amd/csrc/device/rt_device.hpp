@@ -1758,6 +1758,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
             }
             cnt.pe(PH_WAVE_SETUP);
         } else {
+        if (ch > 0 || lead > 0) cnt.pb(PH_WAVE_SETUP);   // (phase builds: a later chunk's test timed from here)
         if constexpr (BV) {
             if ((ch & 63) == 0) {
                 const int c = ch + lane;
@@ -2171,6 +2172,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
     const int nch = BV ? S.n_chunks : (S.n_objs + 63) >> 6;
     uint64_t cm = 0;   // (BV) chunks ch & ~63 .. +63 some querying segment can reach
     for (int ch = 0; ch < nch; ++ch) {
+        if (ch > 0) cnt.pb(PH_WAVE_SETUP);   // (phase builds: a later chunk's test timed from here)
         if constexpr (BV) {
             if ((ch & 63) == 0) {
                 const int c = ch + lane;
@@ -2443,6 +2445,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 if (__float_as_int(S.ctab[2 * o + 1].x) != 0) m |= 1ull << o;
             cnt.pe(PH_WAVE_SETUP);
         } else {
+        if (ch > 0 || lead > 0) cnt.pb(PH_WAVE_SETUP);   // (phase builds: a later chunk's test timed from here)
         if constexpr (BV) {
             if ((ch & 63) == 0) {
                 const int c = ch + lane;
@@ -2828,6 +2831,17 @@ struct WFrame {
     int sf;   // bit 0: stage (0 = reflection child pending, 1 = refraction child pending); bit 1: refraction wanted
 };
 
+// The lead-object path (CompiledScene::n_lead) in trace_wave's closest-hit /
+// shadow queries: off.  Compiled into this kernel its extra code cost the
+// recursion row more than its culling saved (15.33 ms without it in either
+// query, 15.91 with both; profiles/r06_ab/ab_lead_split.txt).  The paper
+// kernel keeps both (4.31-4.34 vs 4.36-4.38 ms).
+#ifndef RT_SEC_LEAD_I
+#define RT_SEC_LEAD_I false
+#endif
+#ifndef RT_SEC_LEAD_S
+#define RT_SEC_LEAD_S false
+#endif
 template <bool EAGER, bool DEEP, bool DL, int WV, class CT>
 __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
     WFrame stk[kMaxDepth];
@@ -2872,7 +2886,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         h.ff = 1;
         if (eval) ++n_isect;
         cnt.pb(PH_PRIMARY);
-        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2), true>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
+        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2), RT_SEC_LEAD_I>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
         cnt.pe(PH_PRIMARY);
         const bool sh = eval && hit;
         // ---- the step's children, pushed before shading (tracer.cpp:38-68)
@@ -2922,7 +2936,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         }
         const V3 wo = normalized(vneg(r.d));
         V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
-        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV, RT_STD_UO, true>(S, ht, h, wo, n_occl, cnt, sh);
+        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV, RT_STD_UO, RT_SEC_LEAD_S>(S, ht, h, wo, n_occl, cnt, sh);
         // the step's value (a finished lane's colour is in memory, so nothing
         // but the stack state is carried across steps)
         V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));

@@ -230,6 +230,12 @@ __device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
 #ifndef RT_PAPER_UO
 #define RT_PAPER_UO true
 #endif
+#ifndef RT_PAPER_LEAD_I   // (A/B switches: lead objects in the paper closest-hit / shadow queries)
+#define RT_PAPER_LEAD_I true
+#endif
+#ifndef RT_PAPER_LEAD_S
+#define RT_PAPER_LEAD_S true
+#endif
 template <bool E, bool D, bool C, bool DL = true, int WV = 0, bool T = false>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     // block 16x16 pixels, wave 8x8
@@ -268,7 +274,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         r = gen_ray(S, x, y);
         ++ni;
         if constexpr (WV)
-            hits = scene_intersect_wave<E, D, (WV == 2), true>(S, r, RV(1e-4), RT_INF, ht, h, __builtin_amdgcn_read_exec() == ~0ull,
+            hits = scene_intersect_wave<E, D, (WV == 2), RT_PAPER_LEAD_I>(S, r, RV(1e-4), RT_INF, ht, h, __builtin_amdgcn_read_exec() == ~0ull,
                                               cnt);
         else
             hits = scene_intersect<E, D>(S, r, RV(1e-4), RT_INF, ht, h, cnt);
@@ -282,7 +288,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     // it mixes shaded rows and neighbour-only rows (strip edges of a
     // multi-GPU partition) or inactive lanes.
     if (__any(sh)) {
-        V3 base = shade<E, D, DL, WV, RT_PAPER_UO, true>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
+        V3 base = shade<E, D, DL, WV, RT_PAPER_UO, RT_PAPER_LEAD_S>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
         if (sh) {
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             band = hatch_band(RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z);
