@@ -219,6 +219,7 @@ template <bool C>
 struct Cnt;
 template <>
 struct Cnt<false> {
+    static constexpr bool kPlain = false;
     __device__ __forceinline__ void inc(int) {}
     __device__ __forceinline__ void gate(bool) {}
 #ifdef RT_EVENT_PROF
@@ -278,6 +279,7 @@ struct Cnt<false> {
 };
 template <>
 struct Cnt<true> {
+    static constexpr bool kPlain = false;
     uint32_t c[16];
     uint32_t on;   // 0 while a lane evaluates an object only to keep the wave convergent
     __device__ __forceinline__ Cnt() : on(1u) {
@@ -292,6 +294,24 @@ struct Cnt<true> {
     __device__ __forceinline__ void pb(int) {}
     __device__ __forceinline__ void pe(int) {}
 };
+// The plain kernels' counter type (no counting, like Cnt<false>): scenes
+// whose objects are all spheres, half-spaces and pokeballs (no transform or
+// CSG object, SceneView::plain) run kernels compiled without the transform /
+// CSG evaluation and the CSG shadow prefilters.  That code, never executed
+// for such scenes, still shaped the register allocation of every path: the
+// paper kernel spilled 48 B/lane and the recursion kernel 48 B beyond its
+// frame stack; without it config 5 runs 4.34 -> 3.78 ms and the recursion row
+// 15.33 -> 12.95 ms (profiles/r06_ab/ab_plain.txt).  The type carries the
+// choice down every query (each is templated on its counter type).
+struct CntPlain : Cnt<false> {
+    static constexpr bool kPlain = true;
+};
+// op-counting builds of a query (Cnt<true>)
+template <class CT>
+constexpr bool kCounting = std::is_same<CT, Cnt<true>>::value;
+// transform / CSG object code compiled in (every kernel but the plain ones)
+template <class CT>
+constexpr bool kCsg = !CT::kPlain;
 
 struct DevScene {
     const NodeT* nodes;
@@ -1324,7 +1344,7 @@ template <bool EAGER, bool DEEP, class CT>
 __device__ __forceinline__ bool object_hit(const DevScene& S, const DevObj& ob, const DRay& world, real tmin,
                                            real tmax, real& t, V3& p, real& ts, int& code, CT& cnt,
                                            uint64_t lmask = ~0ull, bool use_mask = false) {
-    if (ob.kind <= rtamd::OBJ_POKE) {
+    if (!kCsg<CT> || ob.kind <= rtamd::OBJ_POKE) {
         const bool ok = leaf_hit_t(&S.nodes[ob.node], world, tmin, tmax, t, cnt);
         p = ray_at(world, t);
         ts = t;
@@ -1390,7 +1410,7 @@ __device__ __forceinline__ void resolve_hit(const DevScene& S, int obj, const DR
                                             real ts, int code, DHit& h, CT& cnt) {
     const DevObj ob = S.objs[obj];
     h.p = p;
-    if (ob.kind <= rtamd::OBJ_POKE) {
+    if (!kCsg<CT> || ob.kind <= rtamd::OBJ_POKE) {
         leaf_shading(&S.nodes[ob.node], world, p, h, cnt);
         return;
     }
@@ -1768,7 +1788,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
                 cm = (cap && exec_full()) ? __ballot(pass) : ~0ull;
             }
             if (!((cm >> (ch & 63)) & 1ull)) {
-                if constexpr (!std::is_same<CT, Cnt<false>>::value)
+                if constexpr (kCounting<CT>)
                     if (need) cnt_add(cnt, RT_OPC_CULLED, chunk_objects(S, ch << 6));
                 continue;
             }
@@ -1790,7 +1810,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
 #if defined(RT_ABL) && RT_ABL == 2   // diagnostic: setup + transposed test only
         if (m != 12345) return false;
 #endif
-        if constexpr (!std::is_same<CT, Cnt<false>>::value) {
+        if constexpr (kCounting<CT>) {
             if (need) {
                 int skipped = 0;
                 for (int o = base; o < S.n_objs && o < base + 64; ++o) {
@@ -1812,7 +1832,7 @@ __device__ bool scene_occluded_capsule(const DevScene& S, const DRay& r0, real t
             // otherwise the leaves whose balls no querying lane's line meets
             uint64_t lmask = ~0ull;
             bool use_mask = false;
-            if (cap && ob.npb > 0 && exec_full()) {
+            if (kCsg<CT> && cap && ob.npb > 0 && exec_full()) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));
                 const bool in = lane < ob.npb;
                 const uint64_t cb = __ballot(in && capsule_touch(g, K));   // leaves the capsule reaches
@@ -2191,7 +2211,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
                 }
             }
             if (!((cm >> (ch & 63)) & 1ull)) {
-                if constexpr (!std::is_same<CT, Cnt<false>>::value)
+                if constexpr (kCounting<CT>)
                     if (need) cnt_add(cnt, RT_OPC_CULLED, chunk_objects(S, ch << 6));
                 continue;
             }
@@ -2218,7 +2238,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
 #if defined(RT_ABL) && RT_ABL == 2   // diagnostic: setup + transposed test only
         if (m != 12345) return false;
 #endif
-        if constexpr (!std::is_same<CT, Cnt<false>>::value) {
+        if constexpr (kCounting<CT>) {
             if (need) {
                 int skipped = 0;
                 for (int o = base; o < S.n_objs && o < base + 64; ++o) {
@@ -2239,7 +2259,7 @@ __device__ bool scene_occluded_wave(const DevScene& S, const DRay& r0, real tmin
             // otherwise the leaves whose balls no querying lane's line meets
             uint64_t lmask = ~0ull;
             bool use_mask = false;
-            if (cone && ob.npb > 0 && exec_full()) {
+            if (kCsg<CT> && cone && ob.npb > 0 && exec_full()) {
                 const int k = ob.pb0 + (lane < ob.npb ? lane : 0);
                 const float4 g0 = lgb[2 * k], g1 = lgb[2 * k + 1];
                 const bool in = lane < ob.npb;
@@ -2456,7 +2476,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
                 cm = (cone && exec_full()) ? __ballot(pass) : ~0ull;
             }
             if (!((cm >> (ch & 63)) & 1ull)) {
-                if constexpr (!std::is_same<CT, Cnt<false>>::value)
+                if constexpr (kCounting<CT>)
                     if (valid) cnt_add(cnt, RT_OPC_CULLED, chunk_objects(S, ch << 6));
                 continue;
             }
@@ -2471,7 +2491,7 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
         const int nc = S.n_objs - base;
         m = (cone && exec_full()) ? __ballot(pass) : (nc >= 64 ? ~0ull : ((1ull << nc) - 1));
         cnt.pe(PH_WAVE_SETUP);
-        if constexpr (!std::is_same<CT, Cnt<false>>::value) {
+        if constexpr (kCounting<CT>) {
             int skipped = 0;
             for (int o = base; o < S.n_objs && o < base + 64; ++o) {
                 const int k = S.objs[o].kind;
@@ -2492,13 +2512,13 @@ __device__ bool scene_intersect_wave(const DevScene& S, const DRay& r, real tmin
             uint64_t lmask = ~0ull;
 #ifdef RT_NO_LEAF_MASK
             const bool use_mask = false;
-            if (!wide && ob.npb > 0 && exec_full() && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), K))) {
+            if (kCsg<CT> && !wide && ob.npb > 0 && exec_full() && !__any(lane < ob.npb && cone_touch(S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0)), K))) {
                 if (valid) cnt.inc(RT_OPC_CULLED);
                 cnt.pe(PH_OBJ_PREF);
                 continue;
             }
 #else
-            const bool use_mask = !wide && ob.npb > 0 && exec_full();
+            const bool use_mask = kCsg<CT> && !wide && ob.npb > 0 && exec_full();
 #endif
             if (use_mask) {
                 const float* g = S.gb + 4 * (ob.pb0 + (lane < ob.npb ? lane : 0));

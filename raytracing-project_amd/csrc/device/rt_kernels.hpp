@@ -102,8 +102,10 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #define RT_LEAN_WAVES 4
 #endif
 
-template <bool E, bool D, bool SEC, bool C, bool DL = true, int WV = 0>
+// PL: the plain kernels (CntPlain: no transform / CSG code)
+template <bool E, bool D, bool SEC, bool C, bool DL = true, int WV = 0, bool PL = false>
 __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) {
+    static_assert(!(PL && C), "plain kernels do not count");
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int s = lane & 7;
@@ -112,7 +114,7 @@ __device__ __forceinline__ void std_body(const DevScene& S, const StdParams& P) 
     const int ri = blockIdx.y * kStdBlockY + (wave >> 1) * kStdTH + (pix / kStdTW);
     const bool active = x < P.W && ri < P.n_rows;
     uint32_t ni = 0, no = 0;
-    Cnt<C> cnt;
+    std::conditional_t<PL, CntPlain, Cnt<C>> cnt;
     cnt.init();
     V3 c = v3(RV(0.0), RV(0.0), RV(0.0));
     if (active) {
@@ -157,12 +159,16 @@ __global__ __launch_bounds__(kStdThreads) void k_std(DevScene S, StdParams P) {
     std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
+// Occupancy targets of the plain variants (PL; default: the general ones')
+#ifndef RT_PLAIN_LEAN_WAVES
+#define RT_PLAIN_LEAN_WAVES RT_LEAN_WAVES
+#endif
 // WV: 0 = per-lane culls, 1 = wave-level culls, 2 = wave-level culls over the
 // wave BVH (CompiledScene::wobjs / wchunk)
-template <bool C, int WV>
-__global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_LEAN_WAVES))) void k_std_lean(DevScene S,
+template <bool C, int WV, bool PL = false>
+__global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(PL ? RT_PLAIN_LEAN_WAVES : RT_LEAN_WAVES))) void k_std_lean(DevScene S,
                                                                                                        StdParams P) {
-    std_body<false, false, false, C, false, WV>(S, P);
+    std_body<false, false, false, C, false, WV, PL>(S, P);
 }
 
 // Reflection / refraction with wave-level culling (trace_wave): the wave
@@ -170,10 +176,13 @@ __global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_
 #ifndef RT_SEC_WAVES
 #define RT_SEC_WAVES 4
 #endif
-template <bool C, int WV = 1>
-__global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(RT_SEC_WAVES))) void k_std_secw(DevScene S,
+#ifndef RT_PLAIN_SEC_WAVES
+#define RT_PLAIN_SEC_WAVES RT_SEC_WAVES
+#endif
+template <bool C, int WV = 1, bool PL = false>
+__global__ __launch_bounds__(kStdThreads) __attribute__((amdgpu_waves_per_eu(PL ? RT_PLAIN_SEC_WAVES : RT_SEC_WAVES))) void k_std_secw(DevScene S,
                                                                                                       StdParams P) {
-    std_body<false, false, true, C, false, WV>(S, P);   // (no directional lights: those scenes take D)
+    std_body<false, false, true, C, false, WV, PL>(S, P);   // (no directional lights: those scenes take D)
 }
 
 // apply_crosshatch (tracer.cpp:188-205) in two halves.  Its FP64 part - the
@@ -236,8 +245,9 @@ __device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
 #ifndef RT_PAPER_LEAD_S
 #define RT_PAPER_LEAD_S true
 #endif
-template <bool E, bool D, bool C, bool DL = true, int WV = 0, bool T = false>
+template <bool E, bool D, bool C, bool DL = true, int WV = 0, bool T = false, bool PL = false>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
+    static_assert(!(PL && C), "plain kernels do not count");
     // block 16x16 pixels, wave 8x8
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -259,7 +269,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     unsigned t_start = 0u;
     if constexpr (T) t_start = (unsigned)wall_clock64();
     uint32_t ni = 0, no = 0;
-    Cnt<C> cnt;
+    std::conditional_t<PL, CntPlain, Cnt<C>> cnt;
     cnt.init();
     DRay r{v3(RV(0.0), RV(0.0), RV(0.0)), v3(RV(0.0), RV(0.0), -RV(1.0))};
     real ht = RV(0.0);
@@ -321,10 +331,13 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
 #ifndef RT_PAPER_WAVES
 #define RT_PAPER_WAVES RT_LEAN_WAVES
 #endif
-template <bool C, int WV, bool T = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PAPER_WAVES))) void k_paper_primary_lean(
+#ifndef RT_PLAIN_PAPER_WAVES
+#define RT_PLAIN_PAPER_WAVES RT_PAPER_WAVES
+#endif
+template <bool C, int WV, bool T = false, bool PL = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL ? RT_PLAIN_PAPER_WAVES : RT_PAPER_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
-    paper_primary_body<false, false, C, false, WV, T>(S, P);
+    paper_primary_body<false, false, C, false, WV, T, PL>(S, P);
 }
 
 // One paper pixel (tracer.cpp:258-281) from its primary record and its four
@@ -530,6 +543,36 @@ DevScene make_scene(const SceneView& V, bool bv = false) {
     return S;
 }
 
+// The plain kernels (PL) are built for the FP64 namespace only (RT_NO_PLAIN:
+// the FP32 diagnostic build keeps one variant per choice).
+#ifdef RT_NO_PLAIN
+constexpr bool kPlainKernels = false;
+#else
+constexpr bool kPlainKernels = true;
+#endif
+template <int WV>
+void launch_lean(bool c, bool pl, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
+    if (c) hipLaunchKernelGGL((k_std_lean<true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+    else if (kPlainKernels && pl) hipLaunchKernelGGL((k_std_lean<false, WV, kPlainKernels>), grid, dim3(kStdThreads), 0, st, S, P);
+    else hipLaunchKernelGGL((k_std_lean<false, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+}
+template <int WV>
+void launch_secw(bool c, bool pl, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
+    if (c) hipLaunchKernelGGL((k_std_secw<true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+    else if (kPlainKernels && pl) hipLaunchKernelGGL((k_std_secw<false, WV, kPlainKernels>), grid, dim3(kStdThreads), 0, st, S, P);
+    else hipLaunchKernelGGL((k_std_secw<false, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+}
+template <int WV>
+void launch_paper_lean(bool c, bool pl, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
+    // (timed launches: never op-counting ones, rt_frame_trace)
+    if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, WV>), grid, dim3(256), 0, st, S, P);
+    else if (kPlainKernels && pl) {
+        if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, WV, true, kPlainKernels>), grid, dim3(256), 0, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, WV, false, kPlainKernels>), grid, dim3(256), 0, st, S, P);
+    } else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, WV, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary_lean<false, WV>), grid, dim3(256), 0, st, S, P);
+}
+
 template <bool E, bool D, bool SEC, bool WV = false>
 void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
     if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
@@ -559,6 +602,7 @@ void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneVie
     else launch_std_c<true, true, false>(c, grid, st, S, P);
 #else
     const bool wv = V.wave_cull;
+    const bool pl = V.plain != 0;
     if (e) {
         if (sec) launch_std_c<true, true, true>(c, grid, st, S, P);
         else launch_std_c<true, true, false>(c, grid, st, S, P);
@@ -567,24 +611,15 @@ void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const SceneVie
         else launch_std_c<false, true, false>(c, grid, st, S, P);
     } else {
         if (sec) {
-            if (bv) {
-                if (c) hipLaunchKernelGGL((k_std_secw<true, 2>), grid, dim3(kStdThreads), 0, st, S, P);
-                else hipLaunchKernelGGL((k_std_secw<false, 2>), grid, dim3(kStdThreads), 0, st, S, P);
-            } else if (wv) {
-                if (c) hipLaunchKernelGGL((k_std_secw<true>), grid, dim3(kStdThreads), 0, st, S, P);
-                else hipLaunchKernelGGL((k_std_secw<false>), grid, dim3(kStdThreads), 0, st, S, P);
-            } else {
-                launch_std_c<false, false, true>(c, grid, st, S, P);
-            }
+            if (bv) launch_secw<2>(c, pl, grid, st, S, P);
+            else if (wv) launch_secw<1>(c, pl, grid, st, S, P);
+            else launch_std_c<false, false, true>(c, grid, st, S, P);
         } else if (bv) {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, 2>), grid, dim3(kStdThreads), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, 2>), grid, dim3(kStdThreads), 0, st, S, P);
+            launch_lean<2>(c, pl, grid, st, S, P);
         } else if (wv) {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, 1>), grid, dim3(kStdThreads), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, 1>), grid, dim3(kStdThreads), 0, st, S, P);
+            launch_lean<1>(c, pl, grid, st, S, P);
         } else {
-            if (c) hipLaunchKernelGGL((k_std_lean<true, 0>), grid, dim3(kStdThreads), 0, st, S, P);
-            else hipLaunchKernelGGL((k_std_lean<false, 0>), grid, dim3(kStdThreads), 0, st, S, P);
+            launch_lean<0>(c, pl, grid, st, S, P);
         }
     }
 #endif
@@ -599,45 +634,46 @@ void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const Scene
     launch_paper_c<true, true>(c, grid, st, S, P);
 #else
     const bool wv = V.wave_cull;
+    const bool pl = V.plain != 0;
     if (e) launch_paper_c<true, true>(c, grid, st, S, P);
     else if (d) launch_paper_c<false, true>(c, grid, st, S, P);
-    else if (bv) {
-        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 2>), grid, dim3(256), 0, st, S, P);
-        else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, 2, true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary_lean<false, 2>), grid, dim3(256), 0, st, S, P);
-    } else if (wv) {
-        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 1>), grid, dim3(256), 0, st, S, P);
-        else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, 1, true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary_lean<false, 1>), grid, dim3(256), 0, st, S, P);
-    } else {
-        if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, 0>), grid, dim3(256), 0, st, S, P);
-        else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, 0, true>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary_lean<false, 0>), grid, dim3(256), 0, st, S, P);
-    }
+    else if (bv) launch_paper_lean<2>(c, pl, grid, st, S, P);
+    else if (wv) launch_paper_lean<1>(c, pl, grid, st, S, P);
+    else launch_paper_lean<0>(c, pl, grid, st, S, P);
 #endif
 }
 
 // The kernel launch_std / launch_paper pick for a variant (resource queries).
-const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv) {
+const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv, bool pl) {
 #ifdef RT_GENERAL_ONLY
-    (void)e, (void)d, (void)wv, (void)bv;
+    (void)e, (void)d, (void)wv, (void)bv, (void)pl;
     return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
 #else
     if (e) return sec ? (const void*)k_std<true, true, true, false> : (const void*)k_std<true, true, false, false>;
     if (d) return sec ? (const void*)k_std<false, true, true, false> : (const void*)k_std<false, true, false, false>;
-    if (sec) return bv ? (const void*)k_std_secw<false, 2> : wv ? (const void*)k_std_secw<false> : (const void*)k_std<false, false, true, false>;
-    return bv ? (const void*)k_std_lean<false, 2> : wv ? (const void*)k_std_lean<false, 1> : (const void*)k_std_lean<false, 0>;
+    pl = pl && kPlainKernels;
+    if (sec) {
+        if (bv) return pl ? (const void*)k_std_secw<false, 2, kPlainKernels> : (const void*)k_std_secw<false, 2>;
+        if (wv) return pl ? (const void*)k_std_secw<false, 1, kPlainKernels> : (const void*)k_std_secw<false, 1>;
+        return (const void*)k_std<false, false, true, false>;
+    }
+    if (bv) return pl ? (const void*)k_std_lean<false, 2, kPlainKernels> : (const void*)k_std_lean<false, 2>;
+    if (wv) return pl ? (const void*)k_std_lean<false, 1, kPlainKernels> : (const void*)k_std_lean<false, 1>;
+    return pl ? (const void*)k_std_lean<false, 0, kPlainKernels> : (const void*)k_std_lean<false, 0>;
 #endif
 }
 
-const void* paper_kernel(bool e, bool d, bool wv, bool bv) {
+const void* paper_kernel(bool e, bool d, bool wv, bool bv, bool pl) {
 #ifdef RT_GENERAL_ONLY
-    (void)e, (void)d, (void)wv, (void)bv;
+    (void)e, (void)d, (void)wv, (void)bv, (void)pl;
     return (const void*)k_paper_primary<true, true, false>;
 #else
     if (e) return (const void*)k_paper_primary<true, true, false>;
     if (d) return (const void*)k_paper_primary<false, true, false>;
-    return bv ? (const void*)k_paper_primary_lean<false, 2> : wv ? (const void*)k_paper_primary_lean<false, 1> : (const void*)k_paper_primary_lean<false, 0>;
+    pl = pl && kPlainKernels;
+    if (bv) return pl ? (const void*)k_paper_primary_lean<false, 2, false, kPlainKernels> : (const void*)k_paper_primary_lean<false, 2>;
+    if (wv) return pl ? (const void*)k_paper_primary_lean<false, 1, false, kPlainKernels> : (const void*)k_paper_primary_lean<false, 1>;
+    return pl ? (const void*)k_paper_primary_lean<false, 0, false, kPlainKernels> : (const void*)k_paper_primary_lean<false, 0>;
 #endif
 }
 

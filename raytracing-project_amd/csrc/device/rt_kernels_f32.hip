@@ -4,5 +4,6 @@
 // type of the scene records and the trace differs.
 #define RT_REAL float
 #define RT_NS rtf
+#define RT_NO_PLAIN   // (no plain kernel variants in the FP32 diagnostic build)
 #include "rt_device.hpp"
 #include "rt_kernels.hpp"

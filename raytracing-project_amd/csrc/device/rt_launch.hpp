@@ -85,6 +85,7 @@ struct SceneView {
     int n_bounded;
     int wave_cull;   // wave-level culls: cull && n_bounded >= wave_cull_min() (host-decided)
     int n_lead;      // CompiledScene::n_lead (0: none / RT_LEAD=0)
+    int plain;       // only sphere / half-space / pokeball objects: the plain kernels (CntPlain, rt_device.hpp)
     int cam_nx, cam_ny;
     int rec_limit, cull;
     double eye[3], P[3], Lx, Ly;
@@ -168,7 +169,9 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
 
 // Kernel variants (rt_kernels.hpp): E = scene has eager (transform-inside-CSG)
 // objects, D = general compact CSG (deep stacks, directional lights),
-// SEC = reflection/refraction frames, C = op counting.
+// SEC = reflection/refraction frames, C = op counting, pl = plain scene
+// (SceneView::plain: the lean / recursion / paper kernels without transform
+// and CSG code).
 #define RT_DECLARE_LAUNCHERS(NS)                                                                                  \
     namespace NS {                                                                                                \
     void launch_std(bool e, bool d, bool sec, bool c, hipStream_t st, const rtamd::SceneView& V,                 \
@@ -176,8 +179,8 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
     void launch_paper(bool e, bool d, bool c, dim3 grid, hipStream_t st, const rtamd::SceneView& V,               \
                       const rtamd::PaperParams& P);                                                               \
     void launch_paper_finish(dim3 grid, hipStream_t st, const rtamd::PaperParams& P);                             \
-    const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv);                                           \
-    const void* paper_kernel(bool e, bool d, bool wv, bool bv);                                                   \
+    const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv, bool pl);                                  \
+    const void* paper_kernel(bool e, bool d, bool wv, bool bv, bool pl);                                          \
     }
 RT_DECLARE_LAUNCHERS(rtd)
 RT_DECLARE_LAUNCHERS(rtf)

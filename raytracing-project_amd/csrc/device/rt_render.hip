@@ -39,6 +39,18 @@ using rtamd::kMaxRayStack;
 using rtamd::kCounterWords;
 using rtamd::PaperParams;
 using rtamd::SceneView;
+
+namespace {
+// SceneView::plain: every object a sphere, half-space or pokeball (no
+// transform or CSG object: the plain kernels, rt_device.hpp CntPlain)
+bool plain_scene(const rtamd::CompiledScene& cs) {
+    for (const auto& o : cs.objs)
+        if (o.kind != rtamd::OBJ_SPHERE && o.kind != rtamd::OBJ_HALF && o.kind != rtamd::OBJ_POKE &&
+            o.kind != rtamd::OBJ_NEVER && o.kind != rtamd::OBJ_GROUP)
+            return false;
+    return true;
+}
+}  // namespace
 using rtamd::StdParams;
 
 namespace {
@@ -581,6 +593,8 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
     {
         static const bool lead_on = [] { const char* e = std::getenv("RT_LEAD"); return !(e && *e == '0'); }();
         S.n_lead = lead_on ? cs.n_lead : 0;   // (RT_LEAD=0: measurement A/B)
+        static const bool plain_on = [] { const char* e = std::getenv("RT_PLAIN"); return !(e && *e == '0'); }();
+        S.plain = plain_on && plain_scene(cs) ? 1 : 0;   // (RT_PLAIN=0: measurement A/B)
     }
     for (int i = 0; i < 3; ++i) {
         S.eye[i] = d.camera.eye[i];
@@ -1044,7 +1058,7 @@ extern "C" int rt_warmup(int what) {
         // the FP64 render kernels' code object (one per fat binary and
         // device, loaded at its first use; hipFuncGetAttributes loads it)
         hipFuncAttributes a{};
-        HIP_TRY(hipFuncGetAttributes(&a, rtd::std_kernel(false, false, false, true, false)));
+        HIP_TRY(hipFuncGetAttributes(&a, rtd::std_kernel(false, false, false, true, false, false)));
     }
     return RT_OK;
 }
@@ -1438,16 +1452,22 @@ extern "C" int rt_test_kernel_name(const rt_scene* s, int mode, int flags, char*
                                   frames > kMaxDepth);
         const char* ns = big ? "rtdb" : f32 ? "rtf" : "rtd";
         auto tf = [](bool b) { return b ? "true" : "false"; };
+        // (the plain variants: FP64 only, never op-counting)
+        const bool pl = !big && !f32 && !cnt && plain_scene(cs) && [] {
+            const char* e = std::getenv("RT_PLAIN");
+            return !(e && *e == '0');
+        }();
         std::string name;
         if (mode == RT_MODE_PAPER) {
             if (!big && !eager && !deep)
-                name = std::string("k_paper_primary_lean<") + tf(cnt) + ", " + (bv ? "2" : wv ? "1" : "0") + ">";
+                name = std::string("k_paper_primary_lean<") + tf(cnt) + ", " + (bv ? "2" : wv ? "1" : "0") + ", false, " +
+                       tf(pl) + ">";
             else
                 name = std::string("k_paper_primary<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(cnt) + ">";
         } else if (!big && !eager && !deep && !secondary) {
-            name = std::string("k_std_lean<") + tf(cnt) + ", " + (bv ? "2" : wv ? "1" : "0") + ">";
+            name = std::string("k_std_lean<") + tf(cnt) + ", " + (bv ? "2" : wv ? "1" : "0") + ", " + tf(pl) + ">";
         } else if (!big && !eager && !deep && wv) {   // (secondary here)
-            name = std::string("k_std_secw<") + tf(cnt) + ", " + (bv ? "2" : "1") + ">";
+            name = std::string("k_std_secw<") + tf(cnt) + ", " + (bv ? "2" : "1") + ", " + tf(pl) + ">";
         } else {
             name = std::string("k_std<") + tf(big || eager) + ", " + tf(big || deep) + ", " + tf(secondary) + ", " +
                    tf(cnt) + ", false>";
@@ -1481,13 +1501,14 @@ extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32
         const int frames = (secondary && mode == RT_MODE_STANDARD) ? d.recursion_limit - 1 : 0;
         const bool big = !f32 && (cs.max_ray_depth > kMaxRayStack || cs.max_ivl_depth > kMaxIvlSpill + 2 ||
                                   frames > kMaxDepth);
-        const void* fn = big ? (mode == RT_MODE_PAPER ? rtdb::paper_kernel(true, true, false, false)
-                                                      : rtdb::std_kernel(true, true, secondary, false, false))
+        const bool pl = plain_scene(cs);
+        const void* fn = big ? (mode == RT_MODE_PAPER ? rtdb::paper_kernel(true, true, false, false, false)
+                                                      : rtdb::std_kernel(true, true, secondary, false, false, false))
                        : mode == RT_MODE_PAPER
-                             ? (f32 ? rtf::paper_kernel(cs.has_eager, deep, wv, bv)
-                                    : rtd::paper_kernel(cs.has_eager, deep, wv, bv))
-                             : (f32 ? rtf::std_kernel(cs.has_eager, deep, secondary, wv, bv)
-                                    : rtd::std_kernel(cs.has_eager, deep, secondary, wv, bv));
+                             ? (f32 ? rtf::paper_kernel(cs.has_eager, deep, wv, bv, pl)
+                                    : rtd::paper_kernel(cs.has_eager, deep, wv, bv, pl))
+                             : (f32 ? rtf::std_kernel(cs.has_eager, deep, secondary, wv, bv, pl)
+                                    : rtd::std_kernel(cs.has_eager, deep, secondary, wv, bv, pl));
         hipFuncAttributes a{};
         HIP_TRY(hipFuncGetAttributes(&a, fn));
         int blocks = 0;

@@ -1,5 +1,5 @@
-"""The wave BVH kernels (k_std_lean<C, 2>, k_std_secw<C, 2>,
-k_paper_primary_lean<C, 2>: Morton-ordered objects, one transposed test per
+"""The wave BVH kernels (k_std_lean<C, 2, PL>, k_std_secw<C, 2, PL>,
+k_paper_primary_lean<C, 2, T, PL>: Morton-ordered objects, one transposed test per
 64 chunk records before the object tests, closest-hit ties resolved in the
 reference's order; DESIGN.md §Wave BVH) against the reference fixtures
 (tests/golden/bvh.npz, oracle/_ref), the CPU oracle and the same kernels
@@ -30,6 +30,10 @@ def _kernel(rt, sc, mode, flags=0):
     return buf.value.decode()
 
 
+def _wv(name):   # the kernel's wave-cull variant (its second template argument)
+    return name.split("<", 1)[1].split(",")[1].strip()
+
+
 def _render(rt, sc, mode, flags=0):
     st = rt.Stats()
     fb = rt.Tracer(sc, sc.width, sc.height, mode, flags=flags).render(st)
@@ -42,7 +46,7 @@ def _render(rt, sc, mode, flags=0):
 def test_bvh_matches_reference_fixture(gpu, name, mode):
     sc = gpu.load_scene_from_json_text(json.dumps(scenes.bvh_scenes(16)[name]))
     k = _kernel(gpu, sc, mode)
-    assert k.endswith(", 2>"), k   # the BVH variant is the one that runs
+    assert _wv(k) == "2", k   # the BVH variant is the one that runs
     fb, counts = _render(gpu, sc, mode)
     gfb, gcounts = _gold(name, mode)
     d = float(np.abs(fb - gfb).max())
@@ -62,7 +66,7 @@ def test_bvh_equals_no_bvh_and_no_cull(gpu, name, mode):
     result: bit for bit the same frame and ray counts as the wave culls over
     the reference's order, and as no culling at all."""
     sc = gpu.load_scene_from_json_text(json.dumps(scenes.bvh_scenes(16)[name]))
-    assert _kernel(gpu, sc, mode, gpu.RT_FLAG_NO_BVH).endswith(", 1>")
+    assert _wv(_kernel(gpu, sc, mode, gpu.RT_FLAG_NO_BVH)) == "1"
     a, ca = _render(gpu, sc, mode)
     b, cb = _render(gpu, sc, mode, gpu.RT_FLAG_NO_BVH)
     c, cc = _render(gpu, sc, mode, gpu.RT_FLAG_NO_CULL)
@@ -87,7 +91,7 @@ def test_bvh_midres_matches_oracle(gpu, name, dpi):
 def test_bvh_perf_scene_matches_oracle_small(gpu):
     """The 4096-sphere perf scene (tools/bvh_perf.py) at 64x48."""
     sc = gpu.load_scene_from_json_text(json.dumps(scenes.bvh_perf_scene(4096, dpi=16)))
-    assert _kernel(gpu, sc, 0).endswith(", 2>")
+    assert _wv(_kernel(gpu, sc, 0)) == "2"
     fb, counts = _render(gpu, sc, 0)
     ref, ost = gpu.oracle_render(sc, sc.width, sc.height, 0, threads=16)
     assert counts == (int(ost.rays_intersect), int(ost.rays_occluded))
@@ -108,7 +112,7 @@ def test_unbounded_chunk_and_paper_mode(gpu):
     """A floor (unbounded) in its own padded chunk: paper mode of the grid at
     160x120 bit-exact against the oracle, through the BVH kernel."""
     sc = gpu.load_scene_from_json_text(json.dumps(scenes.bvh_scenes(40)["grid"]))
-    assert _kernel(gpu, sc, 1).endswith(", 2>")
+    assert _wv(_kernel(gpu, sc, 1)) == "2"
     fb, counts = _render(gpu, sc, 1)
     ref, ost = gpu.oracle_render(sc, sc.width, sc.height, 1, threads=16)
     assert counts == (int(ost.rays_intersect), int(ost.rays_occluded))
