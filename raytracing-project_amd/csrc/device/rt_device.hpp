@@ -2852,15 +2852,20 @@ struct WFrame {
 };
 
 // The lead-object path (CompiledScene::n_lead) in trace_wave's closest-hit /
-// shadow queries: off.  Compiled into this kernel its extra code cost the
-// recursion row more than its culling saved (15.33 ms without it in either
-// query, 15.91 with both; profiles/r06_ab/ab_lead_split.txt).  The paper
-// kernel keeps both (4.31-4.34 vs 4.36-4.38 ms).
+// shadow queries: on in the plain kernel, off in the general one.  Compiled
+// into the general kernel its extra code cost the recursion row more than its
+// culling saved (15.33 ms without it in either query, 15.91 with both;
+// profiles/r06_ab/ab_lead_split.txt); the plain kernel has the registers for
+// it (12.77 vs 13.00 ms, profiles/r06_ab/ab_plain_tune.txt).  The paper
+// kernels keep both.
 #ifndef RT_SEC_LEAD_I
 #define RT_SEC_LEAD_I false
 #endif
 #ifndef RT_SEC_LEAD_S
 #define RT_SEC_LEAD_S false
+#endif
+#ifndef RT_PLAIN_SEC_LEAD
+#define RT_PLAIN_SEC_LEAD true
 #endif
 template <bool EAGER, bool DEEP, bool DL, int WV, class CT>
 __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n_isect, uint32_t& n_occl, CT& cnt) {
@@ -2906,7 +2911,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         h.ff = 1;
         if (eval) ++n_isect;
         cnt.pb(PH_PRIMARY);
-        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2), RT_SEC_LEAD_I>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
+        const bool hit = scene_intersect_wave<EAGER, DEEP, (WV == 2), kCsg<CT> ? RT_SEC_LEAD_I : RT_PLAIN_SEC_LEAD>(S, r, RV(1e-4), RT_INF, ht, h, wave_ok, cnt, eval);
         cnt.pe(PH_PRIMARY);
         const bool sh = eval && hit;
         // ---- the step's children, pushed before shading (tracer.cpp:38-68)
@@ -2956,7 +2961,7 @@ __device__ __forceinline__ V3 trace_wave(const DevScene& S, DRay r0, uint32_t& n
         }
         const V3 wo = normalized(vneg(r.d));
         V3 direct = v3(RV(0.0), RV(0.0), RV(0.0));
-        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV, RT_STD_UO, RT_SEC_LEAD_S>(S, ht, h, wo, n_occl, cnt, sh);
+        if (__any(sh)) direct = shade<EAGER, DEEP, DL, WV, RT_STD_UO, kCsg<CT> ? RT_SEC_LEAD_S : RT_PLAIN_SEC_LEAD>(S, ht, h, wo, n_occl, cnt, sh);
         // the step's value (a finished lane's colour is in memory, so nothing
         // but the stack state is carried across steps)
         V3 ret = v3(RV(0.0), RV(0.0), RV(0.0));

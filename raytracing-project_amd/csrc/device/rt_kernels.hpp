@@ -159,9 +159,12 @@ __global__ __launch_bounds__(kStdThreads) void k_std(DevScene S, StdParams P) {
     std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
-// Occupancy targets of the plain variants (PL; default: the general ones')
+// Occupancy targets of the plain variants (PL).  The plain lean kernel fits
+// 5 waves/SIMD (config 3 1.11 -> 1.10 ms, config 2 within 1 %); the plain
+// recursion and paper kernels stay at 4 (5: config 6 +0.3 %, config 5 even;
+// profiles/r06_ab/ab_plain_tune.txt).
 #ifndef RT_PLAIN_LEAN_WAVES
-#define RT_PLAIN_LEAN_WAVES RT_LEAN_WAVES
+#define RT_PLAIN_LEAN_WAVES 5
 #endif
 // WV: 0 = per-lane culls, 1 = wave-level culls, 2 = wave-level culls over the
 // wave BVH (CompiledScene::wobjs / wchunk)
