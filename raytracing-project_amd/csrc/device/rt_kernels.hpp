@@ -159,10 +159,13 @@ __global__ __launch_bounds__(kStdThreads) void k_std(DevScene S, StdParams P) {
     std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
-// Occupancy targets of the plain variants (PL).  The plain lean kernel fits
-// 5 waves/SIMD (config 3 1.11 -> 1.10 ms, config 2 within 1 %); the plain
-// recursion and paper kernels stay at 4 (5: config 6 +0.3 %, config 5 even;
-// profiles/r06_ab/ab_plain_tune.txt).
+// Occupancy targets of the plain variants (PL).  The plain lean kernel is
+// compiled for 5 waves/SIMD (config 3 1.11 -> 1.10 ms, config 2 within 1 %):
+// its residency stays at 4 workgroups per CU (the 40 KiB light cache), so
+// the target only tightens its register allocation - a smaller light cache
+// that lets a fifth or sixth workgroup in is slower (config 3 1.22 / 1.35 ms,
+// profiles/r06_ab/ab_light_cache.txt).  The plain recursion and paper kernels
+// stay at 4 (5: config 6 +0.3 %, config 5 even; ab_plain_tune.txt).
 #ifndef RT_PLAIN_LEAN_WAVES
 #define RT_PLAIN_LEAN_WAVES 5
 #endif
