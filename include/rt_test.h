@@ -43,7 +43,8 @@ int rt_test_wave_bvh(const struct rt_scene* s, int32_t* counts, int32_t* worig, 
 
 /* Resources of the trace kernel rt_render would launch for this scene, mode
  * and flags (hipFuncGetAttributes + occupancy query): out[8] = {VGPRs per
- * lane, scratch bytes per lane, static LDS bytes per workgroup, resident
+ * lane, scratch bytes per lane, LDS bytes per workgroup (static + the
+ * dynamic shading pool of 10 KiB per wave), resident
  * workgroups per CU, waves per SIMD, max threads per block, wave-level
  * culling variant, reflection/refraction variant}.  Needs a device. */
 int rt_test_kernel_info(const struct rt_scene* s, int mode, int flags, int32_t* out);

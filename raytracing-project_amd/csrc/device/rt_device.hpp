@@ -2621,22 +2621,27 @@ __device__ __forceinline__ double pow_spec(double x, double y) {
 }
 __device__ __forceinline__ float pow_spec(float x, float y) { return pow(x, y); }
 
-// Per-lane LDS pool of a 256-thread workgroup: shade() keeps pass 1's light
-// geometry (wi, dist) of the first kLightCache lights of each light chunk
-// there for pass 2, instead of recomputing sqrt + three divisions per lit
-// light; flush_counters() reuses the slots of each wave's own lanes at the
-// end.  kLightCache x 4 x 256 doubles = 40 KiB: four workgroups (16 waves)
-// still fit a CU's 160 KiB.  Layout [light][field][thread]: consecutive lanes
-// read consecutive 8-byte words (no bank conflicts).
+// Per-lane LDS pool: shade() keeps pass 1's light geometry (wi, dist) of the
+// first kLightCache lights of each light chunk there for pass 2, instead of
+// recomputing sqrt + three divisions per lit light; flush_counters() reuses
+// each wave's own region at the end.  Every wave owns kPoolWave doubles,
+// laid out [light][field][lane] (consecutive lanes read consecutive 8-byte
+// words: no bank conflicts); the pool is the workgroup's dynamic LDS, sized
+// at launch by pool_bytes(threads) (rt_kernels.hpp launches): kLightCache x 4
+// x 64 doubles = 10 KiB per wave, 40 KiB per 256-thread workgroup, so four
+// workgroups (16 waves) still fit a CU's 160 KiB.
 #ifndef RT_LIGHT_CACHE
 #define RT_LIGHT_CACHE 5
 #endif
 constexpr int kLightCache = RT_LIGHT_CACHE;
-constexpr int kPoolThreads = 256;
+constexpr int kPoolWave = (kLightCache > 0 ? kLightCache : 1) * 4 * 64;
+constexpr size_t pool_bytes(int threads) { return (size_t)(threads / 64) * kPoolWave * sizeof(double); }
 __device__ __forceinline__ double* lds_pool() {
-    __shared__ double pool[(kLightCache > 0 ? kLightCache : 1) * 4 * kPoolThreads];
-    return pool;
+    extern __shared__ double rt_lds_pool[];
+    return rt_lds_pool;
 }
+// wave w's region
+__device__ __forceinline__ double* wave_pool(int w) { return lds_pool() + (size_t)w * kPoolWave; }
 
 __device__ __forceinline__ V3 combine(V3 a, V3 b) {   // shading.cpp:6-12
     return v3(RV(1.0) - (RV(1.0) - a.x) * (RV(1.0) - b.x), RV(1.0) - (RV(1.0) - a.y) * (RV(1.0) - b.y), RV(1.0) - (RV(1.0) - a.z) * (RV(1.0) - b.z));
@@ -2709,7 +2714,7 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
         E = combine(E, combine(Ed, Es));
     }
     if (WV) cnt.pb(PH_SHADE2);   // (pass 2 is timed from the end of pass 1; this start is overwritten)
-    double* const lc = lds_pool() + threadIdx.x;
+    double* const lc = wave_pool((int)(threadIdx.x >> 6)) + (threadIdx.x & 63);
     for (int l0 = 0; __any(valid) && l0 < S.n_lights; l0 += 32) {
         const int l1 = S.n_lights - l0 < 32 ? S.n_lights : l0 + 32;
         uint32_t lit = 0;
@@ -2724,11 +2729,11 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             const auto wq = div3(tl.x, tl.y, tl.z, dist);
             const V3 wi = v3(wq.x, wq.y, wq.z);
             if (li - l0 < kLightCache) {
-                double* c = lc + (li - l0) * 4 * kPoolThreads;
+                double* c = lc + (li - l0) * 4 * 64;
                 c[0] = wi.x;
-                c[kPoolThreads] = wi.y;
-                c[2 * kPoolThreads] = wi.z;
-                c[3 * kPoolThreads] = dist;
+                c[64] = wi.y;
+                c[2 * 64] = wi.z;
+                c[3 * 64] = dist;
             }
             const real ndotl = cmax(RV(0.0), dot3(n, wi));   // (only compared with 0)
             const real max_t = dist - eps;
@@ -2776,9 +2781,9 @@ __device__ V3 shade(const DevScene& S, real ht, const DHit& hit, V3 wo, uint32_t
             V3 wi;
             real dist;
             if (li - l0 < kLightCache) {   // pass 1's values (same lane)
-                const double* c = lc + (li - l0) * 4 * kPoolThreads;
-                wi = v3((real)c[0], (real)c[kPoolThreads], (real)c[2 * kPoolThreads]);
-                dist = (real)c[3 * kPoolThreads];
+                const double* c = lc + (li - l0) * 4 * 64;
+                wi = v3((real)c[0], (real)c[64], (real)c[2 * 64]);
+                dist = (real)c[3 * 64];
             } else {
                 V3 tl = v3(L->pos[0] - hit.p.x, L->pos[1] - hit.p.y, L->pos[2] - hit.p.z);
                 real d2 = dot3(tl, tl);

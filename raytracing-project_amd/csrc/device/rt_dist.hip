@@ -116,11 +116,14 @@ int strip_height(int mode) { return mode == RT_MODE_PAPER ? RT_PAPER_STRIP_ROWS 
 //    slowest of 8 paper-mode ranks 11 % above the mean).
 //  * Rank 0 also places every gathered strip into the frame (the FP64 frame:
 //    24 B/px written; paper mode decodes one byte per pixel into 24), so it
-//    renders fewer strips: weight 1 - c*world (per mille: c = 30 paper, 8
-//    standard, 0 for RGB8 output; from per-rank timings, profiles/r04*).
+//    renders fewer strips: weight 1 - c*world (per mille: c = 45 paper, 8
+//    standard, 0 for RGB8 output; from per-rank timings, profiles/r04*; the
+//    paper value raised 30 -> 45 with the plain paper kernel, whose faster
+//    trace left the root's placement the longest leg: 8-rank frame
+//    0.726 -> 0.708 ms, profiles/r06_ab/ab_dist_shed_plain.txt).
 // The partition is a pure function of (H, world, mode, kind), all of which
 // the ranks check against each other before the first gather.
-constexpr int kRootShedPaper = 30, kRootShedStd = 8;
+constexpr int kRootShedPaper = 45, kRootShedStd = 8;
 // (RT_ROOT_SHED_PAPER / RT_ROOT_SHED_STD: measurement A/B only.  Both values
 // travel in the frame descriptor, so ranks that see different ones refuse the
 // frame together instead of tracing another partition than the root places.)

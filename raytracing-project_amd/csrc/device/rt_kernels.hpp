@@ -28,10 +28,17 @@ namespace {
 // then one atomic per block and counter into one of kCounterSlots slots
 // (blockIdx-hashed).  A single hot address would serialize ~2M atomics at the
 // L2 (~6 ns each, MI355X_MICROARCH.md fan-in row) - 12 ms per 4K frame.
-// Standard-mode workgroup: RT_STD_WPB waves of 4x2 pixels x 8 samples
-// (default 4: 8x4 pixels per 256-thread workgroup).
+// Standard-mode workgroup: RT_STD_WPB waves of 2x4 pixels x 8 samples.
+// Default 1 (round 6): one-wave workgroups, each with its own 10 KiB of
+// dynamic LDS (lds_pool).  A workgroup's LDS is released only when its last
+// wave ends, so with 4-wave workgroups a wave that finished early left its
+// SIMD slot empty until the slowest wave of its group was done; single-wave
+// groups let the dispatcher refill each slot as soon as its wave exits.
+// Measured: recursion row 12.77 -> 10.69 ms (waves of one group take
+// different numbers of bounces), config 4 6.41 -> 6.33 ms
+// (profiles/r06_ab/ab_wpb.txt).
 #ifndef RT_STD_WPB
-#define RT_STD_WPB 4
+#define RT_STD_WPB 1
 #endif
 constexpr int kStdWPB = RT_STD_WPB;
 constexpr int kStdThreads = 64 * kStdWPB;
@@ -54,10 +61,10 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
 #else
     constexpr int NW = C ? 18 : 2;
 #endif
-    // red[w][k] lives in wave w's own lanes' slots of the LDS pool (those
-    // lanes are done with shading when their wave gets here)
-    static_assert(NW <= 64 && NWAVES * 64 <= kPoolThreads, "counter slots");
-    unsigned long long(*red)[64] = reinterpret_cast<unsigned long long(*)[64]>(lds_pool());
+    // red(w)[k] lives in wave w's own region of the LDS pool (its lanes are
+    // done with shading when their wave gets here)
+    static_assert(NW <= 64 && 64 <= kPoolWave, "counter slots");
+    auto red = [](int w) { return reinterpret_cast<unsigned long long*>(wave_pool(w)); };
     unsigned long long v[NW];
     v[0] = ni;
     v[1] = no;
@@ -83,12 +90,12 @@ __device__ __forceinline__ void flush_counters(unsigned long long* ctr, uint32_t
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0)
 #pragma unroll
-        for (int k = 0; k < NW; ++k) red[wave][k] = v[k];
+        for (int k = 0; k < NW; ++k) red(wave)[k] = v[k];
     if constexpr (NWAVES > 1) __syncthreads();
     if (threadIdx.x < NW) {
         unsigned long long sum = 0;
 #pragma unroll
-        for (int w = 0; w < NWAVES; ++w) sum += red[w][threadIdx.x];
+        for (int w = 0; w < NWAVES; ++w) sum += red(w)[threadIdx.x];
         const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x) % kCounterSlots;
         if (sum) atomicAdd(&ctr[(size_t)slot * kCounterWords + threadIdx.x], sum);
     }
@@ -159,15 +166,14 @@ __global__ __launch_bounds__(kStdThreads) void k_std(DevScene S, StdParams P) {
     std_body<E, D, SEC, C, true, WV>(S, P);
 }
 
-// Occupancy targets of the plain variants (PL).  The plain lean kernel is
-// compiled for 5 waves/SIMD (config 3 1.11 -> 1.10 ms, config 2 within 1 %):
-// its residency stays at 4 workgroups per CU (the 40 KiB light cache), so
-// the target only tightens its register allocation - a smaller light cache
-// that lets a fifth or sixth workgroup in is slower (config 3 1.22 / 1.35 ms,
-// profiles/r06_ab/ab_light_cache.txt).  The plain recursion and paper kernels
-// stay at 4 (5: config 6 +0.3 %, config 5 even; ab_plain_tune.txt).
+// Occupancy targets of the plain variants (PL): 4 waves/SIMD (128 VGPRs),
+// as the general kernels.  (A 5-wave target caps the registers at 96 and
+// spills: config 3 1.10 -> 1.22 ms once the LDS pool became dynamic and no
+// longer capped the compiler's occupancy estimate itself; with a static
+// 40 KiB pool the target had been inert, profiles/r06_ab/ab_wpb.txt,
+// ab_light_cache.txt, ab_plain_tune.txt.)
 #ifndef RT_PLAIN_LEAN_WAVES
-#define RT_PLAIN_LEAN_WAVES 5
+#define RT_PLAIN_LEAN_WAVES 4
 #endif
 // WV: 0 = per-lane culls, 1 = wave-level culls, 2 = wave-level culls over the
 // wave BVH (CompiledScene::wobjs / wchunk)
@@ -234,17 +240,38 @@ __device__ __forceinline__ int paper_band(int slot) { return (slot >> 24) & 15; 
 // nothing (a hit's material is an index >= 0, or -1 for none).
 constexpr int kPaperMiss = -3;
 
-// A primary wave's (start, end) tick slot: group-major, 2 * gridDim.x waves
-// (8-column tiles) per 8-entry list group.
-__device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
-    const unsigned w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const unsigned g = blockIdx.y * 2 + (w >> 1), xt = blockIdx.x * 2 + (w & 1);
-    return P.gtime + 2 * ((size_t)g * (2 * gridDim.x) + xt);
-}
+
 
 #ifndef RT_PAPER_UO
 #define RT_PAPER_UO true
 #endif
+// Paper-mode primary workgroup: RT_PAPER_WPB waves of 8x8 pixels (4: 16x16
+// pixels per 256-thread workgroup; 1, the default since round 6: one wave per
+// workgroup with its own 10 KiB of dynamic LDS, as RT_STD_WPB; config 5
+// 3.78 -> 3.56 ms, profiles/r06_ab/ab_wpb.txt).  The host's grid is in 16x16
+// units either way (launch_paper remaps it), and wave (start, end) slots stay
+// per 8x8 tile.
+#ifndef RT_PAPER_WPB
+#define RT_PAPER_WPB 1
+#endif
+constexpr int kPaperWPB = RT_PAPER_WPB;
+static_assert(kPaperWPB == 1 || kPaperWPB == 4, "paper workgroups of 1 or 4 waves");
+constexpr int kPaperThreads = 64 * kPaperWPB;
+// a wave's 8x8 tile: (tile column, list group of 8 entries)
+__device__ __forceinline__ int paper_tile_x() {
+    return kPaperWPB == 4 ? (int)blockIdx.x * 2 + (int)((threadIdx.x >> 6) & 1) : (int)blockIdx.x;
+}
+__device__ __forceinline__ int paper_tile_y() {
+    return kPaperWPB == 4 ? (int)blockIdx.y * 2 + (int)(threadIdx.x >> 7) : (int)blockIdx.y;
+}
+// A primary wave's (start, end) tick slot: group-major, one per 8-column tile
+// (2 * ceil(W / 16) of them, rt_render.hip paper_waves_per_group) per 8-entry
+// list group.
+__device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
+    const unsigned g = __builtin_amdgcn_readfirstlane(paper_tile_y()), xt = __builtin_amdgcn_readfirstlane(paper_tile_x());
+    const unsigned tiles = kPaperWPB == 4 ? 2 * gridDim.x : gridDim.x;
+    return P.gtime + 2 * ((size_t)g * tiles + xt);
+}
 #ifndef RT_PAPER_LEAD_I   // (A/B switches: lead objects in the paper closest-hit / shadow queries)
 #define RT_PAPER_LEAD_I true
 #endif
@@ -254,11 +281,10 @@ __device__ __forceinline__ unsigned* paper_wave_slot(const PaperParams& P) {
 template <bool E, bool D, bool C, bool DL = true, int WV = 0, bool T = false, bool PL = false>
 __device__ __forceinline__ void paper_primary_body(const DevScene& S, const PaperParams& P) {
     static_assert(!(PL && C), "plain kernels do not count");
-    // block 16x16 pixels, wave 8x8
+    // wave 8x8 pixels (block 16x16 or one wave, RT_PAPER_WPB)
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int li = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int x = paper_tile_x() * 8 + (lane & 7);
+    const int li = paper_tile_y() * 8 + (lane >> 3);
     // (list entries < 0 pad a run of consecutive rows to a wave boundary)
     const int ei = li < P.n_list ? P.ext_list[li] : -1;
     const bool active = x < P.W && ei >= 0;
@@ -319,7 +345,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
         P.nz[idx] = h.n.z;
         P.mat[idx] = paper_mat_pack(hits ? h.mat : kPaperMiss, band);
     }
-    flush_counters(P.counters, ni, no, cnt);
+    flush_counters<C, kPaperWPB>(P.counters, ni, no, cnt);
     if constexpr (T) {
         if (__lane_id() == 0) {
             unsigned* slot = paper_wave_slot(P);
@@ -330,7 +356,7 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
 }
 
 template <bool E, bool D, bool C, bool T = false>
-__global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P) {
+__global__ __launch_bounds__(kPaperThreads) void k_paper_primary(DevScene S, PaperParams P) {
     paper_primary_body<E, D, C, true, 0, T>(S, P);
 }
 
@@ -341,7 +367,7 @@ __global__ __launch_bounds__(256) void k_paper_primary(DevScene S, PaperParams P
 #define RT_PLAIN_PAPER_WAVES RT_PAPER_WAVES
 #endif
 template <bool C, int WV, bool T = false, bool PL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PL ? RT_PLAIN_PAPER_WAVES : RT_PAPER_WAVES))) void k_paper_primary_lean(
+__global__ __launch_bounds__(kPaperThreads) __attribute__((amdgpu_waves_per_eu(PL ? RT_PLAIN_PAPER_WAVES : RT_PAPER_WAVES))) void k_paper_primary_lean(
     DevScene S, PaperParams P) {
     paper_primary_body<false, false, C, false, WV, T, PL>(S, P);
 }
@@ -549,6 +575,11 @@ DevScene make_scene(const SceneView& V, bool bv = false) {
     return S;
 }
 
+// Dynamic LDS of the kernels that shade (lds_pool): one region per wave
+constexpr size_t kStdPool = pool_bytes(kStdThreads), kPaperPool = pool_bytes(kPaperThreads);
+// the paper primary's grid from the host's 16x16-pixel units
+inline dim3 pgrid(dim3 g) { return kPaperWPB == 4 ? g : dim3(2 * g.x, 2 * g.y); }
+
 // The plain kernels (PL) are built for the FP64 namespace only (RT_NO_PLAIN:
 // the FP32 diagnostic build keeps one variant per choice).
 #ifdef RT_NO_PLAIN
@@ -558,39 +589,39 @@ constexpr bool kPlainKernels = true;
 #endif
 template <int WV>
 void launch_lean(bool c, bool pl, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std_lean<true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
-    else if (kPlainKernels && pl) hipLaunchKernelGGL((k_std_lean<false, WV, kPlainKernels>), grid, dim3(kStdThreads), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std_lean<false, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_std_lean<true, WV>), grid, dim3(kStdThreads), kStdPool, st, S, P);
+    else if (kPlainKernels && pl) hipLaunchKernelGGL((k_std_lean<false, WV, kPlainKernels>), grid, dim3(kStdThreads), kStdPool, st, S, P);
+    else hipLaunchKernelGGL((k_std_lean<false, WV>), grid, dim3(kStdThreads), kStdPool, st, S, P);
 }
 template <int WV>
 void launch_secw(bool c, bool pl, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std_secw<true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
-    else if (kPlainKernels && pl) hipLaunchKernelGGL((k_std_secw<false, WV, kPlainKernels>), grid, dim3(kStdThreads), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std_secw<false, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_std_secw<true, WV>), grid, dim3(kStdThreads), kStdPool, st, S, P);
+    else if (kPlainKernels && pl) hipLaunchKernelGGL((k_std_secw<false, WV, kPlainKernels>), grid, dim3(kStdThreads), kStdPool, st, S, P);
+    else hipLaunchKernelGGL((k_std_secw<false, WV>), grid, dim3(kStdThreads), kStdPool, st, S, P);
 }
 template <int WV>
 void launch_paper_lean(bool c, bool pl, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
     // (timed launches: never op-counting ones, rt_frame_trace)
-    if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, WV>), grid, dim3(256), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_paper_primary_lean<true, WV>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
     else if (kPlainKernels && pl) {
-        if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, WV, true, kPlainKernels>), grid, dim3(256), 0, st, S, P);
-        else hipLaunchKernelGGL((k_paper_primary_lean<false, WV, false, kPlainKernels>), grid, dim3(256), 0, st, S, P);
-    } else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, WV, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_paper_primary_lean<false, WV>), grid, dim3(256), 0, st, S, P);
+        if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, WV, true, kPlainKernels>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
+        else hipLaunchKernelGGL((k_paper_primary_lean<false, WV, false, kPlainKernels>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
+    } else if (P.gtime) hipLaunchKernelGGL((k_paper_primary_lean<false, WV, true>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary_lean<false, WV>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
 }
 
 template <bool E, bool D, bool SEC, bool WV = false>
 void launch_std_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const StdParams& P) {
-    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true, WV>), grid, dim3(kStdThreads), 0, st, S, P);
-    else hipLaunchKernelGGL((k_std<E, D, SEC, false, WV>), grid, dim3(kStdThreads), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_std<E, D, SEC, true, WV>), grid, dim3(kStdThreads), kStdPool, st, S, P);
+    else hipLaunchKernelGGL((k_std<E, D, SEC, false, WV>), grid, dim3(kStdThreads), kStdPool, st, S, P);
 }
 
 template <bool E, bool D>
 void launch_paper_c(bool c, dim3 grid, hipStream_t st, const DevScene& S, const PaperParams& P) {
     // (timed launches: never op-counting ones, rt_frame_trace)
-    if (c) hipLaunchKernelGGL((k_paper_primary<E, D, true>), grid, dim3(256), 0, st, S, P);
-    else if (P.gtime) hipLaunchKernelGGL((k_paper_primary<E, D, false, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((k_paper_primary<E, D, false>), grid, dim3(256), 0, st, S, P);
+    if (c) hipLaunchKernelGGL((k_paper_primary<E, D, true>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
+    else if (P.gtime) hipLaunchKernelGGL((k_paper_primary<E, D, false, true>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
+    else hipLaunchKernelGGL((k_paper_primary<E, D, false>), pgrid(grid), dim3(kPaperThreads), kPaperPool, st, S, P);
 }
 
 }  // namespace
@@ -668,6 +699,10 @@ const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv, bool pl) {
     return pl ? (const void*)k_std_lean<false, 0, kPlainKernels> : (const void*)k_std_lean<false, 0>;
 #endif
 }
+
+// The trace kernels' workgroup size and dynamic LDS (resource queries)
+int kernel_block_threads(bool paper) { return paper ? kPaperThreads : kStdThreads; }
+size_t kernel_pool_bytes(bool paper) { return paper ? kPaperPool : kStdPool; }
 
 const void* paper_kernel(bool e, bool d, bool wv, bool bv, bool pl) {
 #ifdef RT_GENERAL_ONLY

@@ -181,6 +181,8 @@ constexpr int kCounterSlots = 512;      // spread of the per-block counter atomi
     void launch_paper_finish(dim3 grid, hipStream_t st, const rtamd::PaperParams& P);                             \
     const void* std_kernel(bool e, bool d, bool sec, bool wv, bool bv, bool pl);                                  \
     const void* paper_kernel(bool e, bool d, bool wv, bool bv, bool pl);                                          \
+    int kernel_block_threads(bool paper);                                                                         \
+    size_t kernel_pool_bytes(bool paper);                                                                         \
     }
 RT_DECLARE_LAUNCHERS(rtd)
 RT_DECLARE_LAUNCHERS(rtf)

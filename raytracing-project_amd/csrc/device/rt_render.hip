@@ -1512,12 +1512,17 @@ extern "C" int rt_test_kernel_info(const rt_scene* s, int mode, int flags, int32
         hipFuncAttributes a{};
         HIP_TRY(hipFuncGetAttributes(&a, fn));
         int blocks = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0));
+        const bool paper = mode == RT_MODE_PAPER;
+        const int threads = big ? rtdb::kernel_block_threads(paper)
+                                : f32 ? rtf::kernel_block_threads(paper) : rtd::kernel_block_threads(paper);
+        const size_t pool = big ? rtdb::kernel_pool_bytes(paper)
+                                : f32 ? rtf::kernel_pool_bytes(paper) : rtd::kernel_pool_bytes(paper);
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, threads, pool));
         out[0] = a.numRegs;                      // VGPRs per lane
         out[1] = (int32_t)a.localSizeBytes;      // scratch (spill) bytes per lane
-        out[2] = (int32_t)a.sharedSizeBytes;     // static LDS per workgroup
-        out[3] = blocks;                         // resident 256-thread workgroups per CU
-        out[4] = blocks * 4 / 4;                 // waves per SIMD (4 waves per workgroup, 4 SIMDs per CU)
+        out[2] = (int32_t)(a.sharedSizeBytes + pool);   // LDS per workgroup (static + the shading pool)
+        out[3] = blocks;                                 // resident workgroups per CU
+        out[4] = blocks * (threads / 64) / 4;            // waves per SIMD (4 SIMDs per CU)
         out[5] = a.maxThreadsPerBlock;
         out[6] = wv ? 1 : 0;
         out[7] = secondary ? 1 : 0;

@@ -25,7 +25,7 @@ def strip_for(mode: int) -> int:
     return PAPER_STRIP if mode == 1 else STRIP
 
 
-ROOT_SHED = {0: 8, 1: 30}   # per mille per rank of the root's weight (rt_dist.hip kRootShedStd / kRootShedPaper)
+ROOT_SHED = {0: 8, 1: 45}   # per mille per rank of the root's weight (rt_dist.hip kRootShedStd / kRootShedPaper)
 
 
 def strip_owners(n_strips: int, world: int, mode: int = 0, kind: int = 0) -> list[int]:

@@ -50,6 +50,22 @@ def test_deep_scene_uses_big_stacks(gpu, name):
     assert out[1] < 4096, list(out)    # the bench scene keeps the lean kernel
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,mode", [(4, 0), (3, 0), (5, 1), (5, 0)])
+def test_trace_kernels_carry_their_shading_pool(gpu, cfg, mode):
+    """The light-geometry pool is dynamic LDS sized at launch (10 KiB per
+    wave): the occupancy query sees it, and the trace kernels keep four waves
+    per SIMD."""
+    lib = gpu.amd_lib()
+    lib.rt_test_kernel_info.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int32)]
+    out = (C.c_int32 * 8)()
+    sc = gpu.load_scene_from_json_text(scenes.config_json(cfg, dpi=8)[0])
+    assert lib.rt_test_kernel_info(sc.handle, mode, 0, out) == 0
+    waves_per_group = out[2] // 10240
+    assert waves_per_group >= 1 and out[2] >= 10240 * waves_per_group, list(out)
+    assert out[4] == 4, list(out)
+
+
 def _refused(gpu, text, flags=0):
     sc = gpu.load_scene_from_json_text(text)
     with pytest.raises(gpu.RTError) as e:

@@ -54,7 +54,7 @@ def test_dist_partition(rt, H, world, mode, S):
     n_strips = [sum(1 for o in own if o == r) for r in range(world)]
     if world > 1:
         assert max(n_strips[1:]) - min(n_strips[1:]) <= 1
-        w0 = max(500, 1000 - (30 if mode == 1 else 8) * world) / 1000
+        w0 = max(500, 1000 - frame_dist.ROOT_SHED[mode] * world) / 1000
         assert abs(n_strips[0] - w0 * (len(own) - n_strips[0]) / (world - 1)) <= 1.5
     if mode == 0:
         assert rows == [rt.dist_rows(H, world, r) for r in range(world)]   # rt_dist_rows = standard
