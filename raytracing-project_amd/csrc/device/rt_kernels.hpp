@@ -444,6 +444,48 @@ __device__ __forceinline__ void paper_pixel(const PaperParams& P, int x, int y, 
     dst[2] = o.z;
 }
 
+// A pixel pair's record in one ext row (x even, W even: 8/16-byte loads)
+struct FinRec {
+    int2 m;
+    double2 t, nx, ny, nz;
+};
+__device__ __forceinline__ FinRec fin_load(const PaperParams& P, size_t i) {
+    FinRec r;
+    r.m = *reinterpret_cast<const int2*>(P.mat + i);
+    r.t = *reinterpret_cast<const double2*>(P.t + i);
+    r.nx = *reinterpret_cast<const double2*>(P.nx + i);
+    r.ny = *reinterpret_cast<const double2*>(P.ny + i);
+    r.nz = *reinterpret_cast<const double2*>(P.nz + i);
+    return r;
+}
+// Pixels x and x + 1 of output row ri (frame row y) from the pair's records
+// in the centre (ext index at ci), up and down rows, and their outer
+// x-neighbours (loaded here).
+template <bool CODES>
+__device__ __forceinline__ void paper_finish_pair(const PaperParams& P, int x, int y, int ri, size_t ci, const FinRec& c,
+                                                  const FinRec& u, const FinRec& d) {
+    const size_t li = ci - (x > 0 ? 1 : 0), rj = ci + 1 + (x + 2 < P.W ? 1 : 0);
+    const int ml = paper_mat(P.mat[li]), mr = paper_mat(P.mat[rj]);
+    const real tl = P.t[li], tr = P.t[rj];
+    const real xl = P.nx[li], xr = P.nx[rj], yl = P.ny[li], yr = P.ny[rj], zl = P.nz[li], zr = P.nz[rj];
+    {
+        const int nm[4] = {ml, paper_mat(c.m.y), paper_mat(u.m.x), paper_mat(d.m.x)};
+        const real nt[4] = {tl, RV(c.t.y), RV(u.t.x), RV(d.t.x)};
+        const real nnx[4] = {xl, RV(c.nx.y), RV(u.nx.x), RV(d.nx.x)}, nny[4] = {yl, RV(c.ny.y), RV(u.ny.x), RV(d.ny.x)},
+                   nnz[4] = {zl, RV(c.nz.y), RV(u.nz.x), RV(d.nz.x)};
+        paper_pixel<CODES>(P, x, y, ri, paper_mat(c.m.x), RV(c.t.x), v3(RV(c.nx.x), RV(c.ny.x), RV(c.nz.x)),
+                           paper_band(c.m.x), nm, nt, nnx, nny, nnz);
+    }
+    {
+        const int nm[4] = {paper_mat(c.m.x), mr, paper_mat(u.m.y), paper_mat(d.m.y)};
+        const real nt[4] = {RV(c.t.x), tr, RV(u.t.y), RV(d.t.y)};
+        const real nnx[4] = {RV(c.nx.x), xr, RV(u.nx.y), RV(d.nx.y)}, nny[4] = {RV(c.ny.x), yr, RV(u.ny.y), RV(d.ny.y)},
+                   nnz[4] = {RV(c.nz.x), zr, RV(u.nz.y), RV(d.nz.y)};
+        paper_pixel<CODES>(P, x + 1, y, ri, paper_mat(c.m.y), RV(c.t.y), v3(RV(c.nx.y), RV(c.ny.y), RV(c.nz.y)),
+                           paper_band(c.m.y), nm, nt, nnx, nny, nnz);
+    }
+}
+
 // The finish pass: 64x4 threads per block.  Every operand is loaded up front
 // in one round of independent loads (neighbours outside the frame clamped
 // onto the centre and skipped by paper_pixel; hit/miss is the material slot
@@ -473,41 +515,7 @@ __device__ __forceinline__ void paper_finish_px(const PaperParams& P, int x, int
     } else {
         // rows: c = centre, u = up, d = down; pixels x and x + 1 (x even, W even:
         // every pair is 8/16-byte aligned)
-        const int2 mc = *reinterpret_cast<const int2*>(P.mat + ci);
-        const int2 mu = *reinterpret_cast<const int2*>(P.mat + ui);
-        const int2 md = *reinterpret_cast<const int2*>(P.mat + di);
-        const double2 tc = *reinterpret_cast<const double2*>(P.t + ci);
-        const double2 tu = *reinterpret_cast<const double2*>(P.t + ui);
-        const double2 td = *reinterpret_cast<const double2*>(P.t + di);
-        const double2 xc = *reinterpret_cast<const double2*>(P.nx + ci);
-        const double2 xu = *reinterpret_cast<const double2*>(P.nx + ui);
-        const double2 xd = *reinterpret_cast<const double2*>(P.nx + di);
-        const double2 yc = *reinterpret_cast<const double2*>(P.ny + ci);
-        const double2 yu = *reinterpret_cast<const double2*>(P.ny + ui);
-        const double2 yd = *reinterpret_cast<const double2*>(P.ny + di);
-        const double2 zc = *reinterpret_cast<const double2*>(P.nz + ci);
-        const double2 zu = *reinterpret_cast<const double2*>(P.nz + ui);
-        const double2 zd = *reinterpret_cast<const double2*>(P.nz + di);
-        const size_t li = ci - (x > 0 ? 1 : 0), rj = ci + 1 + (x + 2 < P.W ? 1 : 0);
-        const int ml = paper_mat(P.mat[li]), mr = paper_mat(P.mat[rj]);
-        const real tl = P.t[li], tr = P.t[rj];
-        const real xl = P.nx[li], xr = P.nx[rj], yl = P.ny[li], yr = P.ny[rj], zl = P.nz[li], zr = P.nz[rj];
-        {
-            const int nm[4] = {ml, paper_mat(mc.y), paper_mat(mu.x), paper_mat(md.x)};
-            const real nt[4] = {tl, RV(tc.y), RV(tu.x), RV(td.x)};
-            const real nnx[4] = {xl, RV(xc.y), RV(xu.x), RV(xd.x)}, nny[4] = {yl, RV(yc.y), RV(yu.x), RV(yd.x)},
-                       nnz[4] = {zl, RV(zc.y), RV(zu.x), RV(zd.x)};
-            paper_pixel<CODES>(P, x, y, ri, paper_mat(mc.x), RV(tc.x), v3(RV(xc.x), RV(yc.x), RV(zc.x)), paper_band(mc.x),
-                               nm, nt, nnx, nny, nnz);
-        }
-        {
-            const int nm[4] = {paper_mat(mc.x), mr, paper_mat(mu.y), paper_mat(md.y)};
-            const real nt[4] = {RV(tc.x), tr, RV(tu.y), RV(td.y)};
-            const real nnx[4] = {RV(xc.x), xr, RV(xu.y), RV(xd.y)}, nny[4] = {RV(yc.x), yr, RV(yu.y), RV(yd.y)},
-                       nnz[4] = {RV(zc.x), zr, RV(zu.y), RV(zd.y)};
-            paper_pixel<CODES>(P, x + 1, y, ri, paper_mat(mc.y), RV(tc.y), v3(RV(xc.y), RV(yc.y), RV(zc.y)),
-                               paper_band(mc.y), nm, nt, nnx, nny, nnz);
-        }
+        paper_finish_pair<CODES>(P, x, y, ri, ci, fin_load(P, ci), fin_load(P, ui), fin_load(P, di));
     }
 }
 
@@ -519,7 +527,11 @@ __device__ __forceinline__ void paper_finish_px(const PaperParams& P, int x, int
 #define RT_FINISH_RPT 1
 #endif
 // RT_FINISH_BR rows per block (64 x BR threads): a block's rows share their
-// neighbour rows, only its first and last rows' are read by another block
+// neighbour rows, only its first and last rows' are read by another block.
+// (Measured and rejected in round 6: one wave walking down a 128-pixel column
+// strip, its up / centre / down records kept in registers so that every
+// record row is read once: config 5 3.58 -> 3.65-3.68 ms for 8-32 rows per
+// wave, profiles/r06_ab/ab_finish_walk.txt.)
 #ifndef RT_FINISH_BR
 #define RT_FINISH_BR 4
 #endif
