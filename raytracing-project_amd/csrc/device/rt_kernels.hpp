@@ -245,6 +245,12 @@ constexpr int kPaperMiss = -3;
 #ifndef RT_PAPER_UO
 #define RT_PAPER_UO true
 #endif
+// The plain paper kernel keeps the shadow bundle's wave-uniform parameters in
+// VGPRs (it has the registers: config 5 3.55 -> 3.51 ms,
+// profiles/r06_ab/ab_uo.txt); the general one moves them to SGPRs.
+#ifndef RT_PLAIN_PAPER_UO
+#define RT_PLAIN_PAPER_UO false
+#endif
 // Paper-mode primary workgroup: RT_PAPER_WPB waves of 8x8 pixels (4: 16x16
 // pixels per 256-thread workgroup; 1, the default since round 6: one wave per
 // workgroup with its own 10 KiB of dynamic LDS, as RT_STD_WPB; config 5
@@ -330,7 +336,8 @@ __device__ __forceinline__ void paper_primary_body(const DevScene& S, const Pape
     // it mixes shaded rows and neighbour-only rows (strip edges of a
     // multi-GPU partition) or inactive lanes.
     if (__any(sh)) {
-        V3 base = shade<E, D, DL, WV, RT_PAPER_UO, RT_PAPER_LEAD_S>(S, ht, h, normalized(vneg(r.d)), no, cnt, sh && hits);
+        V3 base = shade<E, D, DL, WV, PL ? RT_PLAIN_PAPER_UO : RT_PAPER_UO, RT_PAPER_LEAD_S>(S, ht, h, normalized(vneg(r.d)), no,
+                                                                                     cnt, sh && hits);
         if (sh) {
             if (!hits) base = v3(RV(1.0), RV(1.0), RV(1.0));
             band = hatch_band(RV(0.299) * base.x + RV(0.587) * base.y + RV(0.114) * base.z);
