@@ -155,6 +155,11 @@ struct FillArgs {
     const rtamd::JRange* R;      // sorted, disjoint output ranges
     const int64_t* segs;         // per workgroup: (segment c, first range overlapping it)
     int8_t parts[MAX_LEVELS];
+    // k_mt_fill_w with ONE range (a whole frame, or one strip): segs = R =
+    // nullptr, the range travels here and workgroup b takes segment c0 + b -
+    // nothing to upload before the fill
+    rtamd::JRange one;
+    int64_t c0;
 };
 
 // Where the draws of one block go: output pair i (outputs bq+2i, bq+2i+1)
@@ -316,12 +321,13 @@ __global__ __launch_bounds__(FILLW_THREADS) void k_mt_fill_w(const uint32_t* __r
                                                              double* __restrict__ jit) {
     __shared__ uint32_t buf[2 * N];
     const int lane = threadIdx.x;
-    const int64_t c = A.segs[2 * blockIdx.x];
-    int r = (int)A.segs[2 * blockIdx.x + 1];
+    const bool one = A.segs == nullptr;   // (kernel-uniform)
+    const int64_t c = one ? A.c0 + blockIdx.x : A.segs[2 * blockIdx.x];
+    int r = one ? 0 : (int)A.segs[2 * blockIdx.x + 1];
     const int64_t seg_q = c * (int64_t)A.K * N;
-    const int64_t q_last = A.R[A.nr - 1].qb;
-    rtamd::JRange g0 = A.R[r];
-    rtamd::JRange g1 = r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
+    const int64_t q_last = one ? A.one.qb : A.R[A.nr - 1].qb;
+    rtamd::JRange g0 = one ? A.one : A.R[r];
+    rtamd::JRange g1 = !one && r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
     for (int k = lane; k < N; k += FILLW_THREADS) buf[k] = table[(size_t)c * N + k];
     lds_barrier();
     int base = 0;
@@ -331,12 +337,12 @@ __global__ __launch_bounds__(FILLW_THREADS) void k_mt_fill_w(const uint32_t* __r
         while (g0.qb <= bq) {   // uniform
             if (++r >= A.nr) break;
             g0 = g1;
-            g1 = r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
+            g1 = !one && r + 1 < A.nr ? A.R[r + 1] : rtamd::JRange{q_last, q_last, 0};
         }
         if (r >= A.nr) break;
         const uint32_t* o = buf + base;
         if (g0.qa < bq + N) {
-            const BlockDst d = block_dst(jit, bq, g0, g1, r, A.nr);
+            const BlockDst d = block_dst(jit, bq, g0, g1, r, A.nr);   // (one range: never generic)
             for (int i = lane; i < N / 2; i += FILLW_THREADS) {
                 double* dst = nullptr;
                 if (d.generic) {
@@ -504,6 +510,18 @@ hipError_t mt_launch_fill(const JitterTable& T, const std::vector<JRange>& range
     }
     const int64_t seg = (int64_t)kTableK * N;
     if ((ranges.back().qb - 1) / seg >= T.n_ck) return hipErrorInvalidValue;   // table too short
+    if (ranges.size() == 1) {
+        // one range: the segments are c0 .. c1, the range goes by value
+        FillArgs F{};
+        F.K = kTableK;
+        F.nr = 1;
+        F.one = ranges[0];
+        F.c0 = ranges[0].qa / seg;
+        const int64_t n_seg = (ranges[0].qb - 1) / seg - F.c0 + 1;
+        job.qmax = ranges[0].qb;
+        hipLaunchKernelGGL(k_mt_fill_w, dim3((unsigned)n_seg), dim3(FILLW_THREADS), 0, stream, T.d_table, F, d_jit);
+        return hipGetLastError();
+    }
     const std::vector<int64_t> segs = job_segments(ranges, seg);
     const size_t b_r = ranges.size() * sizeof(JRange), b_s = segs.size() * sizeof(int64_t);
     job.stage.resize(b_r + b_s);

@@ -197,6 +197,7 @@ struct Workspace {
     // costliest first (order_paper_groups)
     std::map<uint64_t, std::vector<uint32_t>> paper_cost;
     std::vector<rtamd::JRange> jranges;
+    std::vector<int32_t> rows_cached;   // what `rows` holds (a frame with the same rows skips the upload)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
     std::vector<hipEvent_t> pev;   // paper mode: the end of each call's primary pass (pool)
@@ -649,7 +650,12 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         const int64_t q1 = ws.jranges.back().qb;
         HIP_TRY(ws.jit.ensure((size_t)n_rows * 16 * W * sizeof(double)));
         HIP_TRY(ws.jscratch.ensure(rtamd::mt_fill_scratch_bytes(ws.jranges)));
-        HIP_TRY(upload(ws.rows, f->rows_jrow, st, &ws.up));
+        // (the rows / jitter-row lists of the previous frame of this
+        // workspace are still on the device: the same row set skips the copy)
+        if (!(ws.rows.p && ws.rows_cached == f->rows_jrow)) {
+            HIP_TRY(upload(ws.rows, f->rows_jrow, st, &ws.up));
+            ws.rows_cached = f->rows_jrow;
+        }
         ws.jjob.up = &ws.up;
         const auto t_l = SClock::now();
         HIP_TRY(rtamd::mt_launch_fill(ws.jtab, ws.jranges, ws.jjob, ws.jscratch.p, ws.jit.as<double>(), st));
@@ -1154,6 +1160,7 @@ int rtamd::release_device_workspaces(int min_slot) {
                         &w->jscratch, &w->counters, &w->paper_i, &w->paper_d, &w->paper_aux, &w->fb, &w->gtime})
             b->release();
         w->jtab.release();
+        w->rows_cached.clear();
         w->up.release();
         if (w->ctr_host) (void)hipHostFree(w->ctr_host);
         w->ctr_host = nullptr;
