@@ -80,7 +80,7 @@ __global__ void k_to_rgb8(const double* __restrict__ fb, size_t n, uint8_t* __re
 // rt_frame_end reads 144 B after one event instead of copying 72 KiB through
 // the runtime's pageable staging (which waited ~115 us after the last kernel
 // before the copy even started: profiles/r04t_api_timeline.txt).
-__global__ void __launch_bounds__(64) k_reduce_counters(const unsigned long long* __restrict__ slots,
+__global__ void __launch_bounds__(64) k_reduce_counters(unsigned long long* __restrict__ slots,
                                                         unsigned long long* __restrict__ out,
                                                         const unsigned int* __restrict__ gtime, int wpg) {
     // block k < kCounterWords sums word k over the slots (8 independent loads
@@ -98,9 +98,14 @@ __global__ void __launch_bounds__(64) k_reduce_counters(const unsigned long long
         if (lane == 0) reinterpret_cast<unsigned int*>(out + rtamd::kCounterWords)[g] = v;
         return;
     }
+    // (and leaves the slots zero for the next frame: Workspace::counters_zero)
     unsigned long long v = 0;
 #pragma unroll
-    for (int sl = lane; sl < rtamd::kCounterSlots; sl += 64) v += slots[(size_t)sl * rtamd::kCounterWords + k];
+    for (int sl = lane; sl < rtamd::kCounterSlots; sl += 64) {
+        unsigned long long* w = slots + (size_t)sl * rtamd::kCounterWords + k;
+        v += *w;
+        *w = 0ull;
+    }
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) out[k] = v;
 }
@@ -198,6 +203,7 @@ struct Workspace {
     std::map<uint64_t, std::vector<uint32_t>> paper_cost;
     std::vector<rtamd::JRange> jranges;
     std::vector<int32_t> rows_cached;   // what `rows` holds (a frame with the same rows skips the upload)
+    bool counters_zero = false;         // the last frame's k_reduce_counters left `counters` zero (no memset)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> tev;   // one per rt_frame_trace call of the open frame (pool)
     std::vector<hipEvent_t> pev;   // paper mode: the end of each call's primary pass (pool)
@@ -546,8 +552,12 @@ int frame_begin(const rt_scene* s, int W, int H, int mode, int flags, const int3
         for (int i = 0; i < 4; ++i) HIP_TRY(hipEventCreate(&ws.ev[i]));
     }
     const size_t ctr_bytes = (size_t)kCounterSlots * kCounterWords * sizeof(unsigned long long);
-    HIP_TRY(ws.counters.ensure(ctr_bytes));
-    HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
+    {
+        const void* before = ws.counters.p;
+        HIP_TRY(ws.counters.ensure(ctr_bytes));
+        if (!ws.counters_zero || ws.counters.p != before) HIP_TRY(hipMemsetAsync(ws.counters.p, 0, ctr_bytes, st));
+        ws.counters_zero = false;   // (until this frame's reduction has run)
+    }
 
     SceneView& S = f->S;
     S.nodes = fp32 ? ws.nodes_f.p : ws.nodes.p;
@@ -943,13 +953,14 @@ int frame_end_body(rt_frame* f, rt_stats* stats) {
                               hipHostMallocDefault));
         ws.ctr_host_words = host_words;
     }
-    const unsigned long long* ctr = ws.counters.as<unsigned long long>();
+    unsigned long long* ctr = ws.counters.as<unsigned long long>();
     const bool timed = f->timed;   // (some launch of this frame stored its waves' ticks)
     hipLaunchKernelGGL(k_reduce_counters, dim3(kCounterWords + (timed ? n_groups : 0)), dim3(64), 0, st, ctr, ws.ctr_host,
                        ws.gtime.as<unsigned>(), paper_waves_per_group(f->W));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ws.ev[3], st));
     HIP_TRY(rtamd::spin_wait(ws.ev[3]));
+    ws.counters_zero = true;
     unsigned long long hc[kCounterWords];
     for (int k = 0; k < kCounterWords; ++k) hc[k] = ((volatile unsigned long long*)ws.ctr_host)[k];
     if (timed) {
@@ -1161,6 +1172,7 @@ int rtamd::release_device_workspaces(int min_slot) {
             b->release();
         w->jtab.release();
         w->rows_cached.clear();
+        w->counters_zero = false;
         w->up.release();
         if (w->ctr_host) (void)hipHostFree(w->ctr_host);
         w->ctr_host = nullptr;
